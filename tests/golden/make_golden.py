@@ -1,0 +1,337 @@
+"""Capture golden vectors from the real reference DecGridRL.
+
+Runs ONLY in the build container, where the read-only reference checkout is
+mounted at /root/reference.  It imports ``Environments.dec_grid_rl.DecGridRL``
+with two stub modules injected into ``sys.modules`` first:
+  * ``pygame``: ``init`` / ``display.set_mode`` / ``display.update`` no-ops
+    (only used by the ctor and ``render``, ``dec_grid_rl.py:88-89,593-613``);
+  * ``cv2``: only ``distanceTransform`` (DIST_L1, exact) restated with SciPy
+    for the ``dist_reward`` cases (``dec_grid_rl.py:273-275``) — those cases
+    pin the reference's own reward/obs code around that call, while parity
+    with real OpenCV stays unpinned.
+Nothing else of the reference is modified.  The fixtures written here
+(``tests/golden/*.npz``) are inputs + outputs only; the reference itself never
+travels to the GPU box.
+
+    python tests/golden/make_golden.py            # rewrite all fixtures
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("MARLCOV_REFERENCE", "/root/reference")
+
+
+def _install_stubs():
+    pg = types.ModuleType("pygame")
+    pg.init = lambda: None
+    pg.display = types.SimpleNamespace(set_mode=lambda *a, **k: None,
+                                       update=lambda: None)
+    sys.modules["pygame"] = pg
+
+    cv2 = types.ModuleType("cv2")
+    cv2.DIST_L1 = 1
+    cv2.DIST_MASK_PRECISE = 0
+
+    def distanceTransform(src, dist_type, mask):  # exact L1 (taxicab) restatement
+        from scipy.ndimage import distance_transform_cdt
+        assert dist_type == cv2.DIST_L1
+        return distance_transform_cdt(src, metric="taxicab").astype(np.float32)
+
+    cv2.distanceTransform = distanceTransform
+    sys.modules["cv2"] = cv2
+
+
+def _load_reference():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    from Environments.dec_grid_rl import DecGridRL  # noqa: E402
+    from Utils.gridmaker import gridload  # noqa: E402
+    return DecGridRL, gridload
+
+
+BASE = dict(numrobot=1, maxsteps=1000, collision_penalty=5, done_thresh=1,
+            done_incr=0, terminal_reward=30, dist_reward=0, train_maxsteps=1000,
+            test_maxsteps=1000, egoradius=2, mini_map_rad=0, comm_radius=0,
+            allow_comm=0, map_sharing=0, single_square_tool=0, dijkstra_input=0,
+            sensor_type="lidar", sensor_config={"num_lasers": 21, "range": 10})
+
+
+def cfg(**kw):
+    c = dict(BASE)
+    c["sensor_config"] = dict(BASE["sensor_config"])
+    sc = kw.pop("sensor_config", None)
+    if sc is not None:
+        c["sensor_config"] = sc
+    c.update(kw)
+    return c
+
+
+def bernoulli(rs, w, l, p):
+    return rs.choice([1.0, -1.0], size=(w, l), p=[1 - p, p])
+
+
+def tri_valued(rs, w, l):
+    """PNG-style grid: gridload maps 0->-1, 1->0, >=2->1 (gridmaker.py:89-91)."""
+    img = rs.choice([0, 1, 255], size=(w, l), p=[0.15, 0.15, 0.7]).astype(float)
+    return np.clip(img - 1, -1, 1)
+
+
+def handmade(gridload):
+    train, test = gridload(None)
+    return train, test
+
+
+def joint_ints(rs, n, T):
+    """T scalar joint actions: base-4 digits, robot 0 least significant."""
+    out = []
+    for _ in range(T):
+        digits = rs.randint(0, 4, size=n)
+        out.append(("int", int(sum(int(d) * 4 ** i for i, d in enumerate(digits)))))
+    return out
+
+
+def build_cases(gridload):
+    cases = []
+    rs = np.random.RandomState(1234)
+
+    def add(name, config, train, test=None, use_graph=False, seed=0, events=None,
+            even_beams=None):
+        cases.append(dict(name=name, config=config, train=train, test=test,
+                          use_graph=use_graph, seed=seed, events=events,
+                          even_beams=even_beams))
+
+    # C1 plumbing case (BASELINE configs[0]): 1 agent, 32x32 empty, lidar 21/10.
+    T = 200
+    acts = np.random.RandomState(1).randint(4, size=T)
+    add("c1_empty32", cfg(), [np.ones((32, 32))], seed=0,
+        events=[("reset", False, None)] + [("int", int(a)) for a in acts])
+
+    g = bernoulli(rs, 48, 48, 0.2)
+    add("lidar_n4_48", cfg(numrobot=4), [g], seed=3,
+        events=[("reset", False, None)] + joint_ints(rs, 4, 120))
+
+    g = bernoulli(rs, 40, 36, 0.3)
+    add("lidar_even8_r5_nonsquare", cfg(numrobot=3, sensor_config={"num_lasers": 9, "range": 5}),
+        [g], seed=4, even_beams=8,
+        events=[("reset", False, None)] + joint_ints(rs, 3, 100))
+
+    g = bernoulli(rs, 64, 64, 0.1)
+    add("lidar_360_r20", cfg(numrobot=2, sensor_config={"num_lasers": 361, "range": 20}),
+        [g], seed=5, even_beams=360,
+        events=[("reset", False, None)] + joint_ints(rs, 2, 25))
+
+    g = bernoulli(rs, 30, 30, 0.15)
+    add("lidar_frac_range_float_pen",
+        cfg(numrobot=2, collision_penalty=0.5, terminal_reward=2.5,
+            sensor_config={"num_lasers": 13, "range": 7.5}),
+        [g], seed=6, events=[("reset", False, None)] + joint_ints(rs, 2, 60))
+
+    g = bernoulli(rs, 32, 32, 0.2)
+    add("square_r1_n2", cfg(numrobot=2, sensor_type="square_sensor",
+                            sensor_config={"range": 1}),
+        [g], seed=7, events=[("reset", False, None)] + joint_ints(rs, 2, 100))
+
+    train, test = handmade(gridload)
+    ev = []
+    for ind in range(3):
+        ev.append(("reset", True, ind))
+        ev += joint_ints(rs, 1, 60)
+    add("square_r2_single_tool_handmade",
+        cfg(numrobot=1, sensor_type="square_sensor", sensor_config={"range": 2},
+            single_square_tool=1, maxsteps=10000),
+        train, test, seed=8, events=ev)
+
+    g = bernoulli(rs, 40, 40, 0.1)
+    add("comm_graph_n4", cfg(numrobot=4, comm_radius=5, allow_comm=1,
+                             sensor_config={"num_lasers": 21, "range": 6}),
+        [g], use_graph=True, seed=9,
+        events=[("reset", False, None)] + joint_ints(rs, 4, 60))
+
+    g = bernoulli(rs, 40, 40, 0.15)
+    add("map_sharing_n4", cfg(numrobot=4, comm_radius=8, map_sharing=1,
+                              sensor_config={"num_lasers": 15, "range": 6}),
+        [g], seed=10, events=[("reset", False, None)] + joint_ints(rs, 4, 60))
+
+    g = bernoulli(rs, 20, 20, 0.1)
+    add("done_incr", cfg(numrobot=2, done_thresh=0.3, done_incr=0.2,
+                         sensor_config={"num_lasers": 11, "range": 5}),
+        [g], seed=11, events=[("reset", False, None)] + joint_ints(rs, 2, 80))
+
+    g = bernoulli(rs, 30, 30, 0.1)
+    add("maxsteps_hit", cfg(numrobot=1, maxsteps=15, sensor_config={"num_lasers": 7, "range": 3}),
+        [g], seed=12, events=[("reset", False, None)] + joint_ints(rs, 1, 30))
+
+    g = bernoulli(rs, 25, 25, 0.1)
+    ev = [("reset", False, None)]
+    specials = [("int", -1), ("none",), ("int", -2), ("int", -5), ("int", 4 ** 5 + 3),
+                ("int", 12345678901)]
+    for k in range(8):
+        specials.append(("vec", [k]))
+    for t in range(60):
+        ev.append(specials[t % len(specials)] if t % 3 == 0 else ("int", int(rs.randint(4))))
+    add("sentinels_and_odd_actions", cfg(numrobot=1, sensor_config={"num_lasers": 9, "range": 4}),
+        [g], seed=13, events=ev)
+
+    g = bernoulli(rs, 64, 64, 0.1)
+    add("joint_n16", cfg(numrobot=16, sensor_config={"num_lasers": 21, "range": 6}),
+        [g], seed=14, events=[("reset", False, None)] + joint_ints(rs, 16, 15))
+
+    g = tri_valued(rs, 40, 40)
+    add("zero_cells_lidar", cfg(numrobot=3, sensor_config={"num_lasers": 17, "range": 8}),
+        [g], seed=15, events=[("reset", False, None)] + joint_ints(rs, 3, 60))
+    add("zero_cells_square", cfg(numrobot=2, sensor_type="square_sensor",
+                                 sensor_config={"range": 2}),
+        [g], seed=16, events=[("reset", False, None)] + joint_ints(rs, 2, 60))
+
+    ev = []
+    for ind in range(3):
+        ev.append(("reset", True, ind))
+        ev += joint_ints(rs, 1, 40)
+    add("dijkstra_bsa_config",
+        cfg(numrobot=1, egoradius=1, sensor_type="square_sensor", sensor_config={"range": 1},
+            single_square_tool=1, dijkstra_input=1, maxsteps=10000),
+        train, test, seed=17, events=ev)
+
+    g = bernoulli(rs, 32, 32, 0.1)
+    add("dist_reward_lidar", cfg(numrobot=3, dist_reward=1,
+                                 sensor_config={"num_lasers": 21, "range": 6}),
+        [g], seed=18, events=[("reset", False, None)] + joint_ints(rs, 3, 40))
+
+    g = bernoulli(rs, 24, 24, 0.1)
+    add("dist_and_dijkstra_square", cfg(numrobot=2, dist_reward=1, dijkstra_input=1,
+                                        sensor_type="square_sensor", sensor_config={"range": 2}),
+        [g], seed=19, events=[("reset", False, None)] + joint_ints(rs, 2, 30))
+
+    gs = [bernoulli(rs, 20, 20, 0.1) for _ in range(3)]
+    ev = []
+    for _ in range(3):
+        ev.append(("reset", False, None))
+        ev += joint_ints(rs, 2, 30)
+    add("multi_episode_random_grid", cfg(numrobot=2, sensor_config={"num_lasers": 11, "range": 5}),
+        gs, seed=20, events=ev)
+
+    g = bernoulli(rs, 12, 12, 0.3)
+    add("crowded_collisions_n8", cfg(numrobot=8, collision_penalty=2,
+                                     sensor_config={"num_lasers": 9, "range": 4}),
+        [g], seed=21, events=[("reset", False, None)] + joint_ints(rs, 8, 60))
+    return cases
+
+
+def run_case(DecGridRL, case):
+    np.random.seed(case["seed"])
+    env = DecGridRL(case["train"], case["config"], use_graph=case["use_graph"],
+                    test_set=case["test"])
+    if case["even_beams"] is not None:  # lidar.py:11 asserts odd
+        env._sensor._num_lasers = case["even_beams"]
+        env._sensor._thetalist = np.linspace(0, 2 * np.pi, case["even_beams"], endpoint=False)
+    n = env._numrobot
+    rec = {k: [] for k in ("kind", "a_int", "a_vec", "r_testing", "r_ind", "reward", "done",
+                           "obs", "xinds", "yinds", "free", "obst", "robot", "visited",
+                           "adj", "pc", "currstep", "done_thresh", "grid")}
+    comm = bool(env._allow_comm and case["use_graph"])
+    for ev in case["events"]:
+        kind = ev[0]
+        a_int, a_vec, r_t, r_i = 0, np.zeros(n, dtype=np.int64), 0, -1
+        if kind == "reset":
+            out = env.reset(ev[1], ev[2])
+            obs = out[0]
+            reward, done = np.nan, False
+            r_t, r_i = int(bool(ev[1])), (-1 if ev[2] is None else int(ev[2]))
+            code = 3
+        else:
+            if kind == "int":
+                action, code, a_int = ev[1], 0, ev[1]
+            elif kind == "vec":
+                action, code = np.array(ev[1]), 1
+                a_vec[:len(ev[1])] = ev[1]
+            else:
+                action, code = None, 2
+            out = env.step(action)
+            obs = out[0][0] if comm else out[0]
+            reward, done = out[1], out[2]
+            assert isinstance(done, (bool, np.bool_)), type(done)
+        p = env._pad
+        rec["kind"].append(code)
+        rec["a_int"].append(a_int)
+        rec["a_vec"].append(a_vec)
+        rec["r_testing"].append(r_t)
+        rec["r_ind"].append(r_i)
+        rec["reward"].append(float(reward))
+        rec["done"].append(bool(done))
+        rec["obs"].append(np.asarray(obs, dtype=np.float64))
+        rec["xinds"].append(env._xinds.copy())
+        rec["yinds"].append(env._yinds.copy())
+        for key, arr in (("free", env._free_pad), ("obst", env._obst_pad)):
+            assert set(np.unique(arr)) <= {0.0, 1.0}
+            rec[key].append(np.packbits(arr.astype(np.uint8), axis=-1))
+        assert set(np.unique(env._robot_pad)) <= {0.0, 1.0}
+        rec["robot"].append(np.packbits(env._robot_pad.astype(np.uint8), axis=-1))
+        rec["visited"].append(np.packbits(env._visited.astype(np.uint8), axis=-1))
+        rec["adj"].append(env._adjacency_matrix.copy())
+        rec["pc"].append(env.percent_covered())
+        rec["currstep"].append(env._currstep)
+        rec["done_thresh"].append(float(env._done_thresh))
+        rec["grid"].append(env._grid.astype(np.int8))
+        del p
+    return rec
+
+
+def save_case(case, rec):
+    meta = dict(name=case["name"], config=case["config"], use_graph=case["use_graph"],
+                seed=case["seed"], even_beams=case["even_beams"],
+                a_int_digits=[str(e[1]) if e[0] == "int" else "" for e in case["events"]])
+    arrays = dict(meta=np.array(json.dumps(meta)),
+                  train=np.stack([g.astype(np.int8) for g in case["train"]]))
+    if case["test"] is not None:
+        arrays["test"] = np.stack([g.astype(np.int8) for g in case["test"]])
+    for k, v in rec.items():
+        if k == "a_int":
+            continue  # exact ints live in meta (may exceed int64)
+        arrays[k] = np.stack([np.asarray(x) for x in v])
+    path = os.path.join(HERE, f"{case['name']}.npz")
+    np.savez_compressed(path, **arrays)
+    return path
+
+
+def beam_tables():
+    """Golden bits of the per-beam (xinc, yinc, distinc) table, evaluated with
+    the same NumPy scalar expressions as ``lidar.py:38-48``."""
+    out = {}
+    for b in (7, 8, 9, 11, 13, 15, 17, 21, 359, 360, 361, 1001):
+        th = np.linspace(0, 2 * np.pi, num=b, endpoint=False)
+        rows = []
+        for theta in th:
+            xinc = np.cos(theta)
+            yinc = np.sin(theta)
+            larger = max(abs(xinc), abs(yinc))
+            xinc /= larger
+            yinc /= larger
+            rows.append((xinc, yinc, np.sqrt(xinc ** 2 + yinc ** 2)))
+        out[f"b{b}"] = np.array(rows, dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "beam_tables.npz"), **out)
+
+
+def main():
+    DecGridRL, gridload = _load_reference()
+    import contextlib
+    import io
+    beam_tables()
+    total = 0
+    for case in build_cases(gridload):
+        with contextlib.redirect_stdout(io.StringIO()):  # env.done() prints
+            rec = run_case(DecGridRL, case)
+        path = save_case(case, rec)
+        total += os.path.getsize(path)
+        print(f"{case['name']:40s} events={len(case['events']):4d} {os.path.getsize(path)/1024:7.1f} KiB")
+    print(f"total {total/1024:.1f} KiB")
+
+
+if __name__ == "__main__":
+    main()

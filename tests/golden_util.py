@@ -1,0 +1,82 @@
+"""Helpers to load the golden fixtures and replay them through any env class
+with the DecGridRL interface (the CPU oracle or the HIP-backed facade)."""
+from __future__ import annotations
+
+import contextlib
+import glob
+import io
+import json
+import os
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def case_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("beam_tables"))
+
+
+def load_case(name):
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    d["meta"] = json.loads(str(d["meta"]))
+    return d
+
+
+def grids(case, key):
+    if key not in case:
+        return None
+    return [g.astype(np.float64) for g in case[key]]
+
+
+def event_action(case, t):
+    kind = int(case["kind"][t])
+    if kind == 0:
+        return int(case["meta"]["a_int_digits"][t])
+    if kind == 1:
+        n = case["xinds"].shape[1]
+        return np.array(case["a_vec"][t][:max(1, n)])
+    if kind == 2:
+        return None
+    raise ValueError("reset event")
+
+
+def unpack(packed, width):
+    return np.unpackbits(packed, axis=-1)[..., :width]
+
+
+def make_env(env_cls, case, **kw):
+    meta = case["meta"]
+    np.random.seed(meta["seed"])
+    config = dict(meta["config"])
+    if meta["even_beams"] is not None:
+        config["allow_even_beams"] = True
+    with contextlib.redirect_stdout(io.StringIO()):
+        env = env_cls(grids(case, "train"), config, use_graph=meta["use_graph"],
+                      test_set=grids(case, "test"), **kw)
+    if meta["even_beams"] is not None:
+        th = np.linspace(0, 2 * np.pi, meta["even_beams"], endpoint=False)
+        env._sensor.set_thetalist(th)
+    return env
+
+
+def replay(env, case, check, max_events=None):
+    """Replay a golden case; ``check(t, kind, out, case)`` compares step t."""
+    meta = case["meta"]
+    comm = bool(meta["config"]["allow_comm"] and meta["use_graph"])
+    n_ev = len(case["kind"]) if max_events is None else min(max_events, len(case["kind"]))
+    for t in range(n_ev):
+        kind = int(case["kind"][t])
+        with contextlib.redirect_stdout(io.StringIO()):
+            if kind == 3:
+                testing = bool(case["r_testing"][t])
+                ind = int(case["r_ind"][t])
+                out = env.reset(testing, None if ind < 0 else ind)
+                obs, reward, done = out[0], None, None
+            else:
+                out = env.step(event_action(case, t))
+                obs = out[0][0] if comm else out[0]
+                reward, done = out[1], out[2]
+        check(t, kind, dict(obs=obs, reward=reward, done=done, raw=out), case)
