@@ -1,0 +1,229 @@
+"""Throughput benchmark of the batched coverage env step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5] [--envs B]
+
+One "step" = one launch of the HIP env kernel advancing every env of this
+GPU's shard by one timestep (all agents move, sense, merge, reward, done,
+obs, auto-reset).  Inputs (grids, state, per-step action bytes) are resident
+in HBM before the timed region.  N>1: one process per GPU (torchrun), each
+rank owns an independent env shard (weak scaling, no collective on the step
+path); RCCL is used once after timing for the scalar episode-return
+all-reduce and the max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node), 4-agent 128×128 grid, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+BASE = dict(maxsteps=1000, collision_penalty=5, done_thresh=1, done_incr=0, terminal_reward=30,
+            dist_reward=0, train_maxsteps=1000, test_maxsteps=1000, egoradius=2, mini_map_rad=0,
+            comm_radius=0, allow_comm=0, map_sharing=0, single_square_tool=0, dijkstra_input=0,
+            sensor_type="lidar")
+
+# SURVEY.md §8(d) workloads (configs[1] = C2 is the metric's N=1 workload)
+CONFIGS = {
+    "c2": dict(numrobot=4, width=128, sensor_config={"num_lasers": 21, "range": 10}, envs=4096,
+               desc="C2: 4 agents, 128x128 grid p_obst=0.1, lidar 21 beams R=10, egoradius 2"),
+    "c4": dict(numrobot=8, width=256, sensor_config={"num_lasers": 360, "range": 20}, envs=8192,
+               desc="C4: 8 agents, 256x256 grid p_obst=0.1, lidar 360 beams R=20, egoradius 2"),
+}
+
+
+def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3):
+    """per agent s^2 (int8 grid window) + 4*ceil(s^2/8) (free and
+    obst bit windows, read+write) + 2*ceil(s^2/8) (union window read+write) +
+    obs bytes + 1 (action) + 8 (position r/w); per env 32 B."""
+    s = 2 * math.ceil(beam_range) + 1
+    bits = math.ceil(s * s / 8)
+    obs = layers * (2 * ego + 1) ** 2
+    return n_agents * (s * s + 6 * bits + obs + 1 + 8) + 32
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle (NumPy restatement of the reference step, keeping its
+# per-cell Python beam march and full-map copies) in P independent processes.
+# Runs BEFORE the GPU is touched (fork-safe).
+# ---------------------------------------------------------------------------
+def _cpu_worker(args):
+    seed, secs, cfgname = args
+    import numpy as np
+    from oracle.cpu_ref import DecGridRLRef
+
+    c = CONFIGS[cfgname]
+    cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"],
+               allow_even_beams=True)
+    rs = np.random.RandomState(1000 + seed)
+    grid = rs.choice([1.0, -1.0], size=(c["width"], c["width"]), p=[0.9, 0.1])
+    np.random.seed(seed)
+    env = DecGridRLRef([grid], cfg)
+    acts = rs.randint(0, 4, size=(4096, c["numrobot"]))
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        _, _, done = env.step(acts[n % 4096])
+        n += 1
+        if done:
+            env.reset(False, None)
+        if n % 8 == 0 and time.perf_counter() - t0 >= secs:
+            break
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(cfgname, procs, secs):
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(i, secs, cfgname) for i in range(procs)])
+    rate = sum(n / t for n, t in res)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(rate, 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes x {secs:.1f} s, one env each, {CONFIGS[cfgname]['desc']}, "
+                      f"random joint actions; oracle/cpu_ref.py (reference step restated, "
+                      f"per-cell Python beam march kept); host CPU: {cpu}"}
+
+
+def load_traffic(cfgname):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (if any)."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{cfgname}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
+    ap.add_argument("--cpu-procs", type=int, default=8)
+    ap.add_argument("--cpu-secs", type=float, default=2.5)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    c = CONFIGS[args.config]
+    B = args.envs or c["envs"]
+
+    cpu = None
+    if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.config, args.cpu_procs, args.cpu_secs)
+
+    import torch
+    import torch.distributed as dist
+
+    import marlcov
+
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True)
+    N = c["numrobot"]
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
+                                                    seed=1000 + rank, num_grids=B),
+                                   device=dev, seed=1 + rank, auto_reset=True)
+    env.reset()
+    K, W = args.steps, args.warmup
+    g = torch.Generator(device=dev)
+    g.manual_seed(12345 + rank)
+    actions = torch.randint(0, 4, (W + K, B, N), dtype=torch.uint8, device=dev, generator=g)
+    reward_sum = torch.zeros(B, dtype=torch.float64, device=dev)
+    episodes = torch.zeros(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    rp, dp, op = env.reward.data_ptr(), env.done.data_ptr(), env.obs.data_ptr()
+
+    for i in range(W):
+        rc = env.step_raw(actions[i].data_ptr(), rp, dp, op, sp)
+        assert rc == 0, env.lib.mc_last_error()
+    torch.cuda.synchronize(dev)
+    env.check()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(K):
+        starts[i].record(stream)
+        env.step_raw(actions[W + i].data_ptr(), rp, dp, op, sp)
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / K
+    env.check()
+
+    # scalar episode-return statistics: the only collective (outside timing)
+    reward_sum += env.reward
+    episodes += env.done.to(torch.float64)
+    stats = torch.stack([reward_sum.sum(), episodes.sum()])
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    n_gpus = world
+    value = B * n_gpus * K / elapsed
+    bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"])
+    achieved = bpe * B / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.config)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": n_gpus,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64+u64",
+        "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
+        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
+                   "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": 1000},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),
+                     "alg_bytes_per_env_step": bpe},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

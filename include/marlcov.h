@@ -1,0 +1,176 @@
+/*
+ * marlcov.h — C ABI of libmarlcov.so, the MI355X (gfx950) batched coverage
+ * environment.  This is the drop-in boundary for the reference's env hot path
+ * (ExistentialRobotics/MARL-Coverage, Environments/dec_grid_rl.py:DecGridRL).
+ *
+ * The reference has no FFI: its boundary is the duck-typed Python class
+ * DecGridRL (dec_grid_rl.py:21).  Each entry point below replaces one piece of
+ * that class for a whole batch of environments at once; the Python facade
+ * (marl-coverage_amd/dec_grid_rl.py) and the batched env (batch_env.py) bind
+ * them with ctypes.
+ *
+ * Conventions
+ *   - Plain C types only.  `stream` is a hipStream_t passed as void* (NULL =
+ *     the null stream).  Every `dev_*` pointer is HIP device memory owned by
+ *     the caller; env state is owned by the library.
+ *   - Every call returns 0 on success and a negative MC_E* code on error; the
+ *     message is in mc_last_error() (thread-local).  Nothing throws across
+ *     the ABI.  Work is stream-ordered and asynchronous unless noted.
+ *   - One handle per (device, stream); a handle is not thread-safe.
+ *   - Coordinates are in the PADDED grid (the reference pads every map with a
+ *     -1 border, dec_grid_rl.py:471-472): x in [0, width), y in [0, length).
+ */
+#ifndef MARLCOV_H
+#define MARLCOV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MARLCOV_ABI_VERSION 1
+
+enum {
+  MC_OK = 0,
+  MC_EINVAL = -1,   /* bad argument / unsupported config                    */
+  MC_EHIP = -2,     /* HIP runtime error                                     */
+  MC_ESTATE = -3,   /* call out of order (e.g. step before grids)            */
+  MC_EDEVICE = -4   /* a kernel raised its device error word (mc_check)      */
+};
+
+enum { MC_SENSOR_LIDAR = 0, MC_SENSOR_SQUARE = 1 };
+
+/* action byte meanings (per agent), dec_grid_rl.py:131-145 */
+enum {
+  MC_ACT_RIGHT = 0,      /* x + 1 */
+  MC_ACT_UP = 1,         /* y + 1 */
+  MC_ACT_LEFT = 2,       /* x - 1 */
+  MC_ACT_DOWN = 3,       /* y - 1 */
+  /* 4..254: no-op, no penalty (any non-{0,1,2,3} value in the reference)   */
+  MC_ACT_SENTINEL = 255  /* in agent 0's byte: the whole env step is the
+                            reference's `action == None or -1` path
+                            (dec_grid_rl.py:104-107): done=1, reward=0, no
+                            state change, observations still written        */
+};
+
+/* Environment configuration: the reference env_config keys
+ * (dec_grid_rl.py:49-75, lidar.py:8-9, squaresensor.py:12) plus batch extras. */
+typedef struct mc_config {
+  int32_t num_envs;           /* B (batch extra)                              */
+  int32_t num_agents;         /* 'numrobot', 1..64                            */
+  int32_t width;              /* padded grid rows    (unpadded W + 2)         */
+  int32_t length;             /* padded grid columns (unpadded L + 2)         */
+  int32_t num_grids;          /* G grids in the device pool (>= 1)            */
+  int32_t sensor_type;        /* MC_SENSOR_*   ('sensor_type')                */
+  int32_t num_beams;          /* lidar 'num_lasers' (any count >= 1)          */
+  int32_t square_radius;      /* square_sensor 'range'                        */
+  double lidar_range;         /* lidar 'range' (float64 compare, lidar.py:52) */
+  int32_t egoradius;          /* 'egoradius'                                  */
+  int32_t pad;                /* max(egoradius, mini_map_rad) (:78)           */
+  double collision_penalty;   /* 'collision_penalty'                          */
+  double terminal_reward;     /* 'terminal_reward'                            */
+  double done_thresh;         /* 'done_thresh' (initial, per env)             */
+  double done_incr;           /* 'done_incr'                                  */
+  int32_t maxsteps;           /* 'maxsteps' (done when currstep == maxsteps)  */
+  int32_t comm_radius;        /* 'comm_radius' (Chebyshev)                    */
+  int32_t map_sharing;        /* 'map_sharing'                                */
+  int32_t single_square_tool; /* 'single_square_tool'                         */
+  int32_t dist_reward;        /* 'dist_reward'   (must be 0 in ABI v1)        */
+  int32_t dijkstra_input;     /* 'dijkstra_input' (must be 0 in ABI v1)       */
+  int32_t auto_reset;         /* batch extra: re-place agents on done         */
+  int32_t reset_grid_mode;    /* 0: keep the env's grid on reset;
+                                 1: draw a grid uniformly from the pool       */
+  uint64_t seed;              /* batch extra: device Philox seed              */
+} mc_config;
+
+/* Derived geometry (mc_query). */
+typedef struct mc_layout {
+  int32_t words_per_row;      /* ceil(length / 64)                            */
+  int32_t window_half;        /* H: rows/cols staged per agent = 2H+1         */
+  int32_t obs_layers;         /* Lc (3 + dist_reward + dijkstra_input)        */
+  int32_t obs_side;           /* E = 2*egoradius + 1                          */
+  int64_t obs_bytes_per_env;  /* N*Lc*E*E (uint8 obs)                         */
+  int64_t mask_words_per_agent; /* width * words_per_row                       */
+  int64_t state_bytes;        /* device bytes owned by the handle             */
+} mc_layout;
+
+/* State fields for mc_get_state / mc_set_state (device-to-device copies).  */
+enum {
+  MC_FIELD_POS = 0,          /* int32 [B][N][2] (x, y)                         */
+  MC_FIELD_MOVED = 1,        /* uint64 [B]  bit i: robot i is in robot_pad     */
+  MC_FIELD_FREE = 2,         /* uint64 [B][N][width][words_per_row] _free_pad  */
+  MC_FIELD_OBST = 3,         /* uint64 [B][N][width][words_per_row] _obst_pad  */
+  MC_FIELD_VISITED = 4,      /* uint64 [B][width][words_per_row]    _visited   */
+  MC_FIELD_FREE_COUNT = 5,   /* uint32 [B]  count_nonzero(_free_pad > 0)       */
+  MC_FIELD_VISITED_COUNT = 6,/* uint32 [B]  sum(_visited)                      */
+  MC_FIELD_CURRSTEP = 7,     /* int32  [B]  _currstep                          */
+  MC_FIELD_DONE_THRESH = 8,  /* double [B]  _done_thresh                       */
+  MC_FIELD_ENV_GRID = 9,     /* int32  [B]  grid pool index of each env        */
+  MC_FIELD_EPISODE = 10,     /* uint32 [B]  resets so far (RNG counter)        */
+  MC_FIELD_NUMFREE = 11,     /* int32  [G]  count_nonzero(grid > 0) per grid   */
+  MC_FIELD_GRID_NEG = 12,    /* uint64 [G][width][words_per_row] grid < 0      */
+  MC_FIELD_GRID_POS = 13,    /* uint64 [G][width][words_per_row] grid > 0      */
+  MC_FIELD_COUNT = 14
+};
+
+int32_t mc_abi_version(void);
+const char* mc_last_error(void);
+/* sizeof(mc_config) (which=0) / sizeof(mc_layout) (which=1): lets an FFI
+ * binding verify its struct mirror. */
+int64_t mc_struct_size(int32_t which);
+
+/* Allocate device state for cfg->num_envs envs on HIP device `hip_device`.
+ * Replaces DecGridRL.__init__ (dec_grid_rl.py:30-89) minus the first reset. */
+int mc_create(const mc_config* cfg, int hip_device, void** out_env);
+void mc_destroy(void* env);
+int mc_query(void* env, mc_layout* out);
+
+/* Lidar beam table, host memory [num_beams][3] float64 (xinc, yinc, distinc),
+ * computed by the caller exactly as lidar.py:38-48 does (per-theta NumPy
+ * scalar cos/sin, normalise by max(|.|), sqrt).  Synchronous upload. */
+int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams);
+
+/* Upload the grid pool: dev_grids int8 [num_grids][width][length], values
+ * <0 obstacle, 0 traversable-but-not-free, >0 free; the caller has already
+ * added the -1 border.  Replaces the np.pad in reset (dec_grid_rl.py:471). */
+int mc_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void* stream);
+
+/* Synthetic pool: grid g interior cells are obstacles with probability
+ * p_obst (Philox(seed, g)), border -1.  Same distribution as gridgen
+ * (Utils/gridmaker.py:127-128); not the same bits. */
+int mc_generate_grids(void* env, uint64_t seed, double p_obst, void* stream);
+
+/* Which pool grid each env uses (int32 [B], device). */
+int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream);
+
+/* Reset (dec_grid_rl.py:449-531) the envs with dev_env_mask[e] != 0 (NULL =
+ * all).  dev_pos int32 [B][N][2] injects start cells (NULL = device Philox
+ * rejection draw, same acceptance rule as :491-502).  Writes uint8 obs
+ * [B][N][Lc][E][E] for every env (non-reset envs: current-state obs) and,
+ * when dev_adj != NULL, the comm graph uint8 [B][N][N] (:374-391). */
+int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos,
+             void* dev_obs, uint8_t* dev_adj, void* stream);
+
+/* One step of every env (dec_grid_rl.py:91-169) with per-agent action bytes
+ * dev_actions uint8 [B][N] (MC_ACT_*).  Writes reward float64 [B], done uint8
+ * [B], obs uint8 [B][N][Lc][E][E] and optionally the comm graph [B][N][N].
+ * With cfg.auto_reset, an env that reports done is reset in the same launch
+ * and its obs are the first obs of the new episode. */
+int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward,
+            uint8_t* dev_done, void* dev_obs, uint8_t* dev_adj, void* stream);
+
+/* Device-to-device copy of a state field into / out of caller memory.
+ * `bytes` must equal the field size (mc_field_bytes). */
+int64_t mc_field_bytes(void* env, int32_t field);
+int mc_get_state(void* env, int32_t field, void* dev_dst, int64_t bytes, void* stream);
+int mc_set_state(void* env, int32_t field, const void* dev_src, int64_t bytes, void* stream);
+
+/* Synchronise `stream` and report (then clear) the device error word. */
+int mc_check(void* env, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MARLCOV_H */

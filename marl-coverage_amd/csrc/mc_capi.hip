@@ -1,0 +1,426 @@
+// mc_capi.hip — the extern "C" boundary of libmarlcov.so (include/marlcov.h).
+// Owns the device state of a batch of envs and launches mc_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "marlcov.h"
+#include "mc_internal.h"
+
+namespace mc {
+hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
+                      const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
+                      uint8_t* adj, int nt, hipStream_t stream);
+hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream);
+hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
+hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
+}  // namespace mc
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) return fail(MC_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+struct Env {
+  mc_config cfg;
+  mc_layout lay;
+  mc::State s;
+  int device = 0;
+  int nt = 128;
+  bool beams_set = false;
+  bool grids_set = false;
+  std::vector<void*> allocs;
+};
+
+struct FieldDesc {
+  void* ptr;
+  int64_t bytes;
+};
+
+FieldDesc field(Env* E, int f) {
+  const mc::State& s = E->s;
+  const int64_t B = s.B, N = s.N, mw = (int64_t)s.Wp * s.nw, G = s.G;
+  switch (f) {
+    case MC_FIELD_POS: return {s.pos, B * N * 2 * 4};
+    case MC_FIELD_MOVED: return {s.moved, B * 8};
+    case MC_FIELD_FREE: return {s.freem, B * N * mw * 8};
+    case MC_FIELD_OBST: return {s.obstm, B * N * mw * 8};
+    case MC_FIELD_VISITED: return {s.vis, B * mw * 8};
+    case MC_FIELD_FREE_COUNT: return {s.free_cnt, B * 4};
+    case MC_FIELD_VISITED_COUNT: return {s.vis_cnt, B * 4};
+    case MC_FIELD_CURRSTEP: return {s.currstep, B * 4};
+    case MC_FIELD_DONE_THRESH: return {s.done_thresh, B * 8};
+    case MC_FIELD_ENV_GRID: return {s.env_grid, B * 4};
+    case MC_FIELD_EPISODE: return {s.episode, B * 4};
+    case MC_FIELD_NUMFREE: return {(void*)s.numfree, G * 4};
+    case MC_FIELD_GRID_NEG: return {(void*)s.grid_neg, G * mw * 8};
+    case MC_FIELD_GRID_POS: return {(void*)s.grid_pos, G * mw * 8};
+    default: return {nullptr, -1};
+  }
+}
+
+int dev_alloc(Env* E, void** p, size_t bytes) {
+  void* q = nullptr;
+  HIP_TRY(hipMalloc(&q, bytes < 16 ? 16 : bytes));
+  HIP_TRY(hipMemset(q, 0, bytes < 16 ? 16 : bytes));
+  E->allocs.push_back(q);
+  *p = q;
+  return MC_OK;
+}
+
+int env_threads(const mc::State& s) {
+  // enough lanes for the widest phase: beams (lidar), staged rows, union slots
+  int work = s.N * s.Wwin * 2;
+  if (s.sensor == MC_SENSOR_LIDAR) work = work > s.N * s.nbeams ? work : s.N * s.nbeams;
+  if (work <= 64) return 64;
+  if (work <= 128) return 128;
+  if (work <= 1024) return 256;
+  return 512;
+}
+
+Env* as_env(void* p) { return static_cast<Env*>(p); }
+
+}  // namespace
+
+extern "C" {
+
+int32_t mc_abi_version(void) { return MARLCOV_ABI_VERSION; }
+
+const char* mc_last_error(void) { return g_err.c_str(); }
+
+int64_t mc_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(mc_config);
+    case 1: return (int64_t)sizeof(mc_layout);
+    default: return -1;
+  }
+}
+
+int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
+  if (!cfg || !out_env) return fail(MC_EINVAL, "mc_create: null argument");
+  *out_env = nullptr;
+  const mc_config& c = *cfg;
+  if (c.num_envs < 1) return fail(MC_EINVAL, "num_envs must be >= 1 (got %d)", c.num_envs);
+  if (c.num_agents < 1 || c.num_agents > 64)
+    return fail(MC_EINVAL, "numrobot must be in [1, 64] (got %d)", c.num_agents);
+  if (c.width < 3 || c.length < 3 || c.width > 32767 || c.length > 32767)
+    return fail(MC_EINVAL, "padded grid %dx%d out of range", c.width, c.length);
+  if (c.num_grids < 1) return fail(MC_EINVAL, "num_grids must be >= 1");
+  if (c.sensor_type != MC_SENSOR_LIDAR && c.sensor_type != MC_SENSOR_SQUARE)
+    return fail(MC_EINVAL, "unknown sensor_type %d", c.sensor_type);
+  if (c.sensor_type == MC_SENSOR_LIDAR && c.num_beams < 1)
+    return fail(MC_EINVAL, "num_lasers must be >= 1");
+  if (c.sensor_type == MC_SENSOR_SQUARE && c.square_radius < 0)
+    return fail(MC_EINVAL, "square sensor range must be >= 0");
+  if (c.egoradius < 0) return fail(MC_EINVAL, "egoradius must be >= 0");
+  if (c.pad < c.egoradius) return fail(MC_EINVAL, "pad must be >= egoradius");
+  if (c.dist_reward || c.dijkstra_input)
+    return fail(MC_EINVAL, "dist_reward / dijkstra_input layers are not in ABI v1");
+  if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
+
+  int hs = 0;
+  if (c.sensor_type == MC_SENSOR_LIDAR) {
+    // every marked cell is within Chebyshev ceil(range) of the robot: the
+    // major axis moves exactly 1 per step and the fp64 distance sum of
+    // increments >= 1 reaches range after at most ceil(range) steps
+    hs = c.lidar_range > 0 ? (int)ceil(c.lidar_range) : 0;
+    if (c.lidar_range > 31) return fail(MC_EINVAL, "lidar range %g > 31 not supported", c.lidar_range);
+  } else {
+    hs = c.square_radius;
+  }
+  const int H = hs > c.egoradius ? hs : c.egoradius;
+  if (2 * H + 1 > 63)
+    return fail(MC_EINVAL, "window 2H+1 = %d exceeds 63 (range/egoradius too large)", 2 * H + 1);
+
+  Env* E = new Env();
+  E->cfg = c;
+  E->device = hip_device;
+  mc::State& s = E->s;
+  s.B = c.num_envs;
+  s.N = c.num_agents;
+  s.Wp = c.width;
+  s.Lp = c.length;
+  s.nw = (c.length + 63) / 64;
+  s.G = c.num_grids;
+  s.H = H;
+  s.Wwin = 2 * H + 1;
+  s.ego = c.egoradius;
+  s.E = 2 * c.egoradius + 1;
+  s.Lc = 3;
+  s.sensor = c.sensor_type;
+  s.nbeams = c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0;
+  s.sq_r = c.square_radius;
+  s.range = c.lidar_range;
+  s.pen = c.collision_penalty;
+  s.term = c.terminal_reward;
+  s.dincr = c.done_incr;
+  s.maxsteps = c.maxsteps;
+  s.comm_r = c.comm_radius;
+  s.sst = c.single_square_tool ? 1 : 0;
+  s.auto_reset = c.auto_reset ? 1 : 0;
+  s.grid_mode = c.reset_grid_mode;
+  s.seed = c.seed;
+
+  hipError_t he = hipSetDevice(hip_device);
+  if (he != hipSuccess) {
+    delete E;
+    return fail(MC_EHIP, "hipSetDevice(%d): %s", hip_device, hipGetErrorString(he));
+  }
+  const size_t B = s.B, N = s.N, mw = (size_t)s.Wp * s.nw, G = s.G;
+  void* p = nullptr;
+  int rc = MC_OK;
+  size_t total = 0;
+#define ALLOC(dst, T, count)                                  \
+  do {                                                        \
+    if (rc == MC_OK) rc = dev_alloc(E, &p, (count) * sizeof(T)); \
+    dst = (T*)p;                                              \
+    total += (count) * sizeof(T);                             \
+  } while (0)
+  uint64_t *gneg = nullptr, *gpos = nullptr;
+  int32_t* nfree = nullptr;
+  double* beams = nullptr;
+  ALLOC(gneg, uint64_t, G * mw);
+  ALLOC(gpos, uint64_t, G * mw);
+  ALLOC(nfree, int32_t, G);
+  ALLOC(beams, double, (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 3);
+  ALLOC(s.env_grid, int32_t, B);
+  ALLOC(s.pos, int32_t, B * N * 2);
+  ALLOC(s.moved, uint64_t, B);
+  ALLOC(s.freem, uint64_t, B * N * mw);
+  ALLOC(s.obstm, uint64_t, B * N * mw);
+  ALLOC(s.vis, uint64_t, B * mw);
+  ALLOC(s.free_cnt, uint32_t, B);
+  ALLOC(s.vis_cnt, uint32_t, B);
+  ALLOC(s.currstep, int32_t, B);
+  ALLOC(s.done_thresh, double, B);
+  ALLOC(s.episode, uint32_t, B);
+  ALLOC(s.err, uint32_t, 4);
+#undef ALLOC
+  s.grid_neg = gneg;
+  s.grid_pos = gpos;
+  s.numfree = nfree;
+  s.beams = beams;
+  if (rc != MC_OK) {
+    std::string msg = g_err;
+    mc_destroy(E);
+    return fail(rc, "%s", msg.c_str());
+  }
+  {
+    std::vector<int32_t> eg(B);
+    for (size_t i = 0; i < B; ++i) eg[i] = (int32_t)(i % G);
+    std::vector<double> dt(B, c.done_thresh);
+    if (hipMemcpy(s.env_grid, eg.data(), B * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s.done_thresh, dt.data(), B * 8, hipMemcpyHostToDevice) != hipSuccess) {
+      mc_destroy(E);
+      return fail(MC_EHIP, "mc_create: initial upload failed");
+    }
+  }
+  E->nt = env_threads(s);
+  mc_layout& L = E->lay;
+  L.words_per_row = s.nw;
+  L.window_half = s.H;
+  L.obs_layers = s.Lc;
+  L.obs_side = s.E;
+  L.obs_bytes_per_env = (int64_t)N * s.Lc * s.E * s.E;
+  L.mask_words_per_agent = (int64_t)mw;
+  L.state_bytes = (int64_t)total;
+  if (s.sensor != MC_SENSOR_LIDAR) E->beams_set = true;
+  *out_env = E;
+  return MC_OK;
+}
+
+void mc_destroy(void* env) {
+  Env* E = as_env(env);
+  if (!E) return;
+  (void)hipSetDevice(E->device);
+  for (void* p : E->allocs) (void)hipFree(p);
+  delete E;
+}
+
+int mc_query(void* env, mc_layout* out) {
+  if (!env || !out) return fail(MC_EINVAL, "mc_query: null argument");
+  *out = as_env(env)->lay;
+  return MC_OK;
+}
+
+int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
+  Env* E = as_env(env);
+  if (!E || !host_table) return fail(MC_EINVAL, "mc_set_beam_table: null argument");
+  if (E->s.sensor != MC_SENSOR_LIDAR) return fail(MC_EINVAL, "beam table on a non-lidar env");
+  if (num_beams < 1) return fail(MC_EINVAL, "beam table needs >= 1 beam");
+  for (int b = 0; b < num_beams; ++b) {
+    const double xi = host_table[3 * b], yi = host_table[3 * b + 1], di = host_table[3 * b + 2];
+    if (!(fabs(xi) <= 1.0 && fabs(yi) <= 1.0 && di >= 1.0 && (fabs(xi) == 1.0 || fabs(yi) == 1.0)))
+      return fail(MC_EINVAL, "beam %d is not a normalised lidar.py increment (%g, %g, %g)", b, xi,
+                  yi, di);
+  }
+  HIP_TRY(hipSetDevice(E->device));
+  if (num_beams != E->s.nbeams) {
+    // the reference lets callers swap _thetalist after construction
+    // (even beam counts); re-size the device table
+    HIP_TRY(hipDeviceSynchronize());
+    void* nb = nullptr;
+    HIP_TRY(hipMalloc(&nb, (size_t)num_beams * 3 * sizeof(double)));
+    for (auto& p : E->allocs)
+      if (p == (void*)E->s.beams) { (void)hipFree(p); p = nb; }
+    E->s.beams = (const double*)nb;
+    E->s.nbeams = num_beams;
+    E->cfg.num_beams = num_beams;
+    E->nt = env_threads(E->s);
+  }
+  HIP_TRY(hipMemcpy((void*)E->s.beams, host_table, (size_t)num_beams * 3 * sizeof(double),
+                    hipMemcpyHostToDevice));
+  E->beams_set = true;
+  return MC_OK;
+}
+
+static int check_numfree(Env* E, hipStream_t st) {
+  std::vector<int32_t> nf(E->s.G);
+  HIP_TRY(hipMemcpyAsync(nf.data(), E->s.numfree, nf.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int g = 0; g < E->s.G; ++g)
+    if (nf[g] <= 0)
+      return fail(MC_EINVAL,
+                  "grid %d has no cell > 0: the reference's percent_covered() divides by "
+                  "count_nonzero(grid > 0) (dec_grid_rl.py:552)",
+                  g);
+  E->grids_set = true;
+  return MC_OK;
+}
+
+int mc_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_grids) return fail(MC_EINVAL, "mc_set_grids: null argument");
+  if (num_grids != E->s.G)
+    return fail(MC_EINVAL, "mc_set_grids: %d grids, config says %d", num_grids, E->s.G);
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemsetAsync((void*)E->s.numfree, 0, (size_t)E->s.G * 4, st));
+  HIP_TRY(mc::launch_pack(E->s, dev_grids, st));
+  return check_numfree(E, st);
+}
+
+int mc_generate_grids(void* env, uint64_t seed, double p_obst, void* stream) {
+  Env* E = as_env(env);
+  if (!E) return fail(MC_EINVAL, "mc_generate_grids: null env");
+  if (!(p_obst >= 0.0 && p_obst < 1.0)) return fail(MC_EINVAL, "p_obst must be in [0, 1)");
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemsetAsync((void*)E->s.numfree, 0, (size_t)E->s.G * 4, st));
+  HIP_TRY(mc::launch_gen(E->s, seed, p_obst, st));
+  return check_numfree(E, st);
+}
+
+int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_env_grid) return fail(MC_EINVAL, "mc_set_env_grids: null argument");
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemcpyAsync(E->s.env_grid, dev_env_grid, (size_t)E->s.B * 4, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return MC_OK;
+}
+
+static int ready(Env* E, const char* who) {
+  if (!E->beams_set) return fail(MC_ESTATE, "%s: lidar beam table not set (mc_set_beam_table)", who);
+  if (!E->grids_set) return fail(MC_ESTATE, "%s: grids not set (mc_set_grids / mc_generate_grids)", who);
+  return MC_OK;
+}
+
+int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, void* dev_obs,
+             uint8_t* dev_adj, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_obs) return fail(MC_EINVAL, "mc_reset: null argument");
+  int rc = ready(E, "mc_reset");
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(mc::launch_env(E->s, mc::MODE_RESET, nullptr, dev_env_mask, dev_pos, nullptr, nullptr,
+                         (uint8_t*)dev_obs, dev_adj, E->nt, (hipStream_t)stream));
+  return MC_OK;
+}
+
+int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
+            void* dev_obs, uint8_t* dev_adj, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_actions || !dev_reward || !dev_done || !dev_obs)
+    return fail(MC_EINVAL, "mc_step: null argument");
+  int rc = ready(E, "mc_step");
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(E->device));
+  if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
+  HIP_TRY(mc::launch_env(E->s, mc::MODE_STEP, dev_actions, nullptr, nullptr, dev_reward, dev_done,
+                         (uint8_t*)dev_obs, dev_adj, E->nt, st));
+  return MC_OK;
+}
+
+int64_t mc_field_bytes(void* env, int32_t f) {
+  Env* E = as_env(env);
+  if (!E) return fail(MC_EINVAL, "mc_field_bytes: null env");
+  FieldDesc d = field(E, f);
+  if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
+  return d.bytes;
+}
+
+int mc_get_state(void* env, int32_t f, void* dev_dst, int64_t bytes, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_dst) return fail(MC_EINVAL, "mc_get_state: null argument");
+  FieldDesc d = field(E, f);
+  if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
+  if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemcpyAsync(dev_dst, d.ptr, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MC_OK;
+}
+
+int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_src) return fail(MC_EINVAL, "mc_set_state: null argument");
+  FieldDesc d = field(E, f);
+  if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
+  if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  if (f == MC_FIELD_GRID_NEG || f == MC_FIELD_GRID_POS || f == MC_FIELD_NUMFREE) E->grids_set = true;
+  return MC_OK;
+}
+
+int mc_check(void* env, void* stream) {
+  Env* E = as_env(env);
+  if (!E) return fail(MC_EINVAL, "mc_check: null env");
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(E->device));
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpyAsync(&err, E->s.err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (err) {
+    HIP_TRY(hipMemsetAsync(E->s.err, 0, 4, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return fail(MC_EDEVICE, "device error word 0x%x (1=window 2=out-of-grid 4=placement 8=inject)", err);
+  }
+  return MC_OK;
+}
+
+}  // extern "C"

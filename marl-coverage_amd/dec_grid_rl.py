@@ -1,0 +1,302 @@
+"""DecGridRL: drop-in facade of the reference environment, stepped on the GPU.
+
+Same constructor, methods, attributes and return types as
+``Environments/dec_grid_rl.py:DecGridRL`` (ExistentialRobotics/MARL-Coverage),
+so the reference's controllers and episode loop (``Utils/utils.py``) run
+unchanged.  Every step is one launch of the HIP env kernel (batch of 1); the
+host keeps only what the reference's callers read back.
+
+Randomness is the reference's: ``reset`` draws the grid index and the robot
+start cells from NumPy's global RNG with the same call sequence
+(dec_grid_rl.py:466-502), then injects the cells into the device env, so a
+seeded run reproduces the reference's trajectory bit for bit.
+
+Differences (deliberate supersets): per-agent action arrays/lists are accepted
+for any ``numrobot`` (the reference raises ValueError on them for N > 1,
+SURVEY §8(a) a1); ``render`` returns the composed RGB frame without pygame.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .batch_env import BatchCoverageEnv, pad_grid
+from .sensors import make_sensor
+
+_DIRS = (0, 1, 2, 3)
+
+
+def decode_action(action, numrobot):
+    """Reference action decoding (dec_grid_rl.py:104-117) -> uint8 codes [N].
+
+    Returns None for the sentinel (``action == None or action == -1``)."""
+    if action is None:
+        return None
+    if isinstance(action, (list, tuple)):
+        action = np.asarray(action)
+    if isinstance(action, np.ndarray):
+        flat = action.reshape(-1)
+        if flat.size == 1 and flat[0] == -1:
+            return None
+        ulis = flat
+    else:
+        try:
+            if action == -1:
+                return None
+        except Exception:
+            pass
+        ulis = np.zeros((numrobot,))
+        for i in range(numrobot):
+            ulis[i] = action % 4
+            action = action // 4
+    codes = np.full(numrobot, _lib.ACT_NOOP, dtype=np.uint8)
+    for i in range(min(numrobot, len(ulis))):
+        u = ulis[i]
+        for d in _DIRS:
+            if u == d:
+                codes[i] = d
+                break
+    return codes
+
+
+class DecGridRL:
+    """GPU-backed ``DecGridRL(train_set, env_config, use_graph, test_set)``."""
+
+    def __init__(self, train_set, env_config, use_graph=False, test_set=None, device="cuda"):
+        import torch
+
+        self._torch = torch
+        self._train_gridlis = train_set
+        self._test_gridlis = test_set
+        c = env_config
+        self._env_config = dict(env_config)
+        self._numrobot = c["numrobot"]
+        self._maxsteps = c["maxsteps"]
+        self._collision_penalty = c["collision_penalty"]
+        self._dt = c["done_thresh"]           # host mirror of the device value
+        self._done_incr = c["done_incr"]
+        self._terminal_reward = c["terminal_reward"]
+        self._dist_r = c["dist_reward"]
+        self._train_maxsteps = c["train_maxsteps"]
+        self._test_maxsteps = c["test_maxsteps"]
+        self._egoradius = c["egoradius"]
+        self._mini_map_rad = c["mini_map_rad"]
+        self._comm_radius = c["comm_radius"]
+        self._allow_comm = c["allow_comm"]
+        self._map_sharing = c["map_sharing"]
+        self._use_graph = use_graph
+        self._single_square_tool = c["single_square_tool"]
+        self._dijkstra_input = c["dijkstra_input"]
+        self._sensor = make_sensor(c)
+        self._pad = max(self._egoradius, self._mini_map_rad)
+        self._device = torch.device(device)
+        self._envs = {}          # padded shape -> (BatchCoverageEnv, [pool grid ids])
+        self._pool_index = {}    # id(grid) -> (shape, index)
+        self._env = None
+        self.reset(False, None)
+        self._obs_dim = self.get_egocentric_observations()[0].shape
+        self._num_actions = 4
+
+    # ---- device env per padded grid shape ----------------------------------
+    def _device_env(self, grid):
+        padded_shape = (grid.shape[0] + 2, grid.shape[1] + 2)
+        if padded_shape not in self._envs:
+            pool = [g for g in list(self._train_gridlis or []) + list(self._test_gridlis or [])
+                    if np.asarray(g).shape == grid.shape]
+            uniq, seen = [], set()
+            for g in pool:
+                if id(g) not in seen:
+                    seen.add(id(g))
+                    uniq.append(g)
+            if not any(g is grid for g in uniq):
+                uniq.append(grid)
+            env = BatchCoverageEnv(self._env_config, 1, grids=uniq, device=self._device,
+                                   auto_reset=False, sensor=self._sensor,
+                                   want_adjacency=True)
+            self._envs[padded_shape] = (env, uniq)
+        env, uniq = self._envs[padded_shape]
+        idx = next(i for i, g in enumerate(uniq) if g is grid)
+        return env, idx
+
+    def _push_done_thresh(self, env):
+        t = self._torch.tensor([float(self._dt)], dtype=self._torch.float64)
+        env.set_state(_lib.FIELD_DONE_THRESH, t)
+
+    @property
+    def _done_thresh(self):
+        """``_done_thresh`` persists across resets and grows by done_incr each
+        time done() fires (dec_grid_rl.py:52,542); the device holds it."""
+        return self._dt
+
+    @_done_thresh.setter
+    def _done_thresh(self, value):
+        self._dt = value
+        if getattr(self, "_env", None) is not None:
+            self._push_done_thresh(self._env)
+
+    # ---- reference API ------------------------------------------------------
+    def reset(self, testing, ind):
+        """``dec_grid_rl.py:449-531`` (same NumPy RNG call sequence)."""
+        if testing and self._test_gridlis is not None:
+            raw = self._test_gridlis[ind]
+        else:
+            raw = self._train_gridlis[np.random.randint(len(self._train_gridlis))]
+        grid = pad_grid(raw)
+        self._grid = grid
+        self._gridwidth, self._gridlen = grid.shape
+        self._currstep = 0
+        n = self._numrobot
+        xs = np.zeros(n, dtype=int)
+        ys = np.zeros(n, dtype=int)
+        taken = np.zeros(grid.shape, dtype=bool)
+        count = 0
+        while count != n:
+            x = np.random.randint(self._gridwidth)
+            y = np.random.randint(self._gridlen)
+            if grid[x][y] >= 0 and not taken[x][y]:
+                taken[x][y] = True
+                xs[count], ys[count] = x, y
+                count += 1
+        env, idx = self._device_env(np.asarray(raw))
+        if self._env is not env:
+            self._env = env
+            self._push_done_thresh(env)
+        env.set_env_grids([idx])
+        pos = np.stack([xs, ys], axis=1)[None].astype(np.int32)
+        env.reset(positions=pos)
+        self._xinds, self._yinds = xs, ys
+        self._robot_pos_map = taken.astype(np.float64)
+        self._numfree = int(np.count_nonzero(grid > 0))
+        self._numobserved = 0
+        self._refresh(reset=True)
+        obs = self._obs_np
+        if self._allow_comm and self._use_graph:
+            return obs, self._grid, self._adjacency_matrix
+        return obs, self._grid
+
+    def step(self, action):
+        """``dec_grid_rl.py:91-169``."""
+        env = self._env
+        codes = decode_action(action, self._numrobot)
+        sentinel = codes is None
+        a = np.full((1, self._numrobot), _lib.ACT_SENTINEL if sentinel else 0, dtype=np.uint8)
+        if not sentinel:
+            a[0] = codes
+        env.step(self._torch.from_numpy(a).to(env.device))
+        self._refresh(reset=False)
+        if sentinel:
+            reward, done = 0, True
+        else:
+            reward = np.float64(self._reward_dev)
+            done = bool(self._done_dev)
+        obs = self._obs_np
+        if self._allow_comm and self._use_graph:
+            return [obs, self._adjacency_matrix], reward, done
+        return obs, reward, done
+
+    def _refresh(self, reset):
+        env = self._env
+        torch = self._torch
+        obs = env.obs[0].to("cpu", non_blocking=False)
+        self._obs_np = obs.numpy().astype(np.float64)
+        pos = env.get_state(_lib.FIELD_POS)[0].cpu().numpy()
+        self._xinds = pos[:, 0].astype(int)
+        self._yinds = pos[:, 1].astype(int)
+        self._adjacency_matrix = env.adj[0].cpu().numpy().astype(np.float64)
+        self._currstep = int(env.get_state(_lib.FIELD_CURRSTEP)[0].item())
+        dt = float(env.get_state(_lib.FIELD_DONE_THRESH)[0].item())
+        if dt != float(self._dt):
+            self._dt = dt
+        if not reset:
+            self._reward_dev = float(env.reward[0].item())
+            self._done_dev = int(env.done[0].item())
+        rp = np.zeros(self._grid.shape)
+        rp[self._xinds, self._yinds] = 1
+        self._robot_pos_map = rp
+        del torch
+
+    def get_egocentric_observations(self):
+        return self._obs_np.copy()
+
+    def percent_covered(self):
+        """``dec_grid_rl.py:548-552``."""
+        fc = int(self._env.get_state(_lib.FIELD_FREE_COUNT)[0].item())
+        return fc / self._numfree
+
+    def done(self):
+        """``dec_grid_rl.py:533-546`` (without the print)."""
+        if min(self._done_thresh, 1) <= self.percent_covered():
+            self._done_thresh += self._done_incr
+            self._push_done_thresh(self._env)
+            return True
+        if self._currstep == self._maxsteps:
+            return True
+        return False
+
+    def isInBounds(self, x, y):
+        return x >= 0 and x < self._gridwidth and y >= 0 and y < self._gridlen
+
+    def isOccupied(self, x, y):
+        return self._grid[x][y] < 0 or self._robot_pos_map[x][y] == 1
+
+    # ---- reference state arrays, materialised from the device on demand ----
+    def _unpack(self, words):
+        W, L = self._gridwidth, self._gridlen
+        w = words.cpu().numpy().astype(np.uint64)
+        bits = np.unpackbits(w.view(np.uint8).reshape(w.shape[:-1] + (-1,)), axis=-1,
+                             bitorder="little")[..., :L]
+        return bits.reshape(w.shape[:-2] + (W, L)).astype(np.float64)
+
+    def _padded(self, inner):
+        p = self._pad
+        pad = [(0, 0)] * (inner.ndim - 2) + [(p, p), (p, p)]
+        return np.pad(inner, pad)
+
+    @property
+    def _free_pad(self):
+        return self._padded(self._unpack(self._env.get_state(_lib.FIELD_FREE)[0]))
+
+    @property
+    def _obst_pad(self):
+        return self._padded(self._unpack(self._env.get_state(_lib.FIELD_OBST)[0]))
+
+    @property
+    def _visited(self):
+        return self._unpack(self._env.get_state(_lib.FIELD_VISITED)[0])
+
+    @property
+    def _observed_obstacles(self):
+        return np.clip(self._unpack(self._env.get_state(_lib.FIELD_OBST)[0]).sum(axis=0), 0, 1)
+
+    @property
+    def _robot_pad(self):
+        moved = int(self._env.get_state(_lib.FIELD_MOVED)[0].item()) & ((1 << 64) - 1)
+        rp = np.zeros((self._gridwidth + 2 * self._pad, self._gridlen + 2 * self._pad))
+        for i in range(self._numrobot):
+            if (moved >> i) & 1:
+                rp[self._xinds[i] + self._pad, self._yinds[i] + self._pad] = 1
+        return rp
+
+    def render(self):
+        """RGB frame of ``dec_grid_rl.py:561-580`` (no pygame / cv2 scaling)."""
+        image = np.zeros((self._gridwidth, self._gridlen, 3))
+        ob = self._observed_obstacles
+        image += np.stack([200 * ob, 0 * ob, 255 * ob], -1)
+        vis = self._visited
+        image += np.stack([0 * vis, 225 * vis, 255 * vis], -1)
+        rp = self._robot_pos_map
+        image += np.stack([255 * rp, 0 * rp, 0 * rp], -1)
+        return image
+
+    def snapshot(self):
+        """Comparable state (same keys as the oracle's snapshot())."""
+        return {
+            "xinds": self._xinds.copy(), "yinds": self._yinds.copy(),
+            "free_pad": (self._free_pad > 0).astype(np.uint8),
+            "obst_pad": (self._obst_pad > 0).astype(np.uint8),
+            "robot_pad": (self._robot_pad > 0).astype(np.uint8),
+            "visited": (self._visited > 0).astype(np.uint8),
+            "adjacency": self._adjacency_matrix.copy(),
+            "currstep": int(self._currstep),
+            "done_thresh": float(self._dt),
+        }

@@ -318,11 +318,23 @@ def beam_tables():
     np.savez_compressed(os.path.join(HERE, "beam_tables.npz"), **out)
 
 
+def handmade_data(gridload):
+    """The reference's hand-made 15x15 grids (gridmaker.py:23-80) as package
+    data for marl-coverage_amd/gridmaker.py:gridload(None)."""
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        train, test = gridload(None)
+    out = os.path.join(HERE, "..", "..", "marl-coverage_amd", "data", "handmade15.npz")
+    np.savez_compressed(out, train=np.stack(train).astype(np.int8), test=np.stack(test).astype(np.int8))
+
+
 def main():
     DecGridRL, gridload = _load_reference()
     import contextlib
     import io
     beam_tables()
+    handmade_data(gridload)
     total = 0
     for case in build_cases(gridload):
         with contextlib.redirect_stdout(io.StringIO()):  # env.done() prints

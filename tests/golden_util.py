@@ -80,3 +80,34 @@ def replay(env, case, check, max_events=None):
                 obs = out[0][0] if comm else out[0]
                 reward, done = out[1], out[2]
         check(t, kind, dict(obs=obs, reward=reward, done=done, raw=out), case)
+
+
+def check_against_golden(env):
+    """Bit-exact comparison of env (oracle or facade) with the golden record."""
+    def check(t, kind, out, case):
+        tag = f"{case['meta']['name']} event {t} kind {kind}"
+        np.testing.assert_array_equal(np.asarray(out["obs"], dtype=np.float64), case["obs"][t],
+                                      err_msg=tag + " obs")
+        if kind != 3:
+            r = float(out["reward"])
+            assert r == case["reward"][t], (tag, r, case["reward"][t])
+            assert bool(out["done"]) == bool(case["done"][t]), tag
+        np.testing.assert_array_equal(env._xinds, case["xinds"][t], err_msg=tag)
+        np.testing.assert_array_equal(env._yinds, case["yinds"][t], err_msg=tag)
+        snap = env.snapshot()
+        for key, gkey in (("free_pad", "free"), ("obst_pad", "obst"), ("robot_pad", "robot"),
+                          ("visited", "visited")):
+            np.testing.assert_array_equal(np.packbits(snap[key], axis=-1), case[gkey][t],
+                                          err_msg=f"{tag} {key}")
+        np.testing.assert_array_equal(snap["adjacency"], case["adj"][t], err_msg=tag + " adj")
+        assert env.percent_covered() == case["pc"][t], tag
+        assert snap["currstep"] == case["currstep"][t], tag
+        assert snap["done_thresh"] == case["done_thresh"][t], tag
+        np.testing.assert_array_equal(env._grid.astype(np.int8), case["grid"][t], err_msg=tag)
+    return check
+
+
+def needs_layers(case):
+    """Golden cases using obs layers not in ABI v1 (dist_reward / dijkstra)."""
+    c = case["meta"]["config"]
+    return bool(c.get("dist_reward")) or bool(c.get("dijkstra_input"))

@@ -1,0 +1,252 @@
+"""GPU parity: the HIP path (libmarlcov.so through its C ABI) against the CPU
+oracle and the reference's golden vectors.  Bit-exact on masks, positions,
+obs, done and counters; rewards compared exactly (tolerance 0: every reward
+term is an integer-valued or config-valued float64 added in reference order,
+well inside north_star's 1e-6)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from golden_util import case_names, check_against_golden, load_case, make_env, needs_layers, replay
+from gpu_util import compare_env, device_state, oracle_from_device, ref_action
+from oracle.cpu_ref import DecGridRLRef
+
+pytestmark = pytest.mark.gpu
+
+REWARD_TOL = 0.0  # north_star allows 1e-6; the build is exact
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+def base_cfg(**kw):
+    c = dict(numrobot=1, maxsteps=1000, collision_penalty=5, done_thresh=1, done_incr=0,
+             terminal_reward=30, dist_reward=0, train_maxsteps=1000, test_maxsteps=1000,
+             egoradius=2, mini_map_rad=0, comm_radius=0, allow_comm=0, map_sharing=0,
+             single_square_tool=0, dijkstra_input=0, sensor_type="lidar",
+             sensor_config={"num_lasers": 21, "range": 10})
+    c.update(kw)
+    return c
+
+
+# ---------------------------------------------------------------------------
+# 1. the DecGridRL facade replays every golden case of the reference
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", case_names())
+def test_facade_matches_reference_golden(torch_cuda, name):
+    import marlcov
+    case = load_case(name)
+    if needs_layers(case):
+        pytest.skip("dist_reward / dijkstra obs layers are not in the HIP path yet (SURVEY 8f)")
+    env = make_env(marlcov.DecGridRL, case)
+    replay(env, case, check_against_golden(env))
+
+
+# ---------------------------------------------------------------------------
+# 2. batched env vs one oracle env per batch entry, random actions
+# ---------------------------------------------------------------------------
+def bern(rs, w, l, p):
+    return rs.choice([1.0, -1.0], size=(w, l), p=[1 - p, p])
+
+
+def tri(rs, w, l):
+    return rs.choice([-1.0, 0.0, 1.0], size=(w, l), p=[0.15, 0.15, 0.7])
+
+
+BATCH_CASES = {
+    # name: (config, grid maker, B, T)
+    "c2_like_n4_128": (base_cfg(numrobot=4), lambda rs: bern(rs, 128, 128, 0.1), 12, 30),
+    "c4_like_n8_256_360beams": (base_cfg(numrobot=8, allow_even_beams=True,
+                                         sensor_config={"num_lasers": 360, "range": 20}),
+                                lambda rs: bern(rs, 256, 256, 0.1), 3, 6),
+    "nonsquare_70x150_r12": (base_cfg(numrobot=5, sensor_config={"num_lasers": 31, "range": 12}),
+                             lambda rs: bern(rs, 70, 150, 0.2), 8, 25),
+    "frac_range_float_pen": (base_cfg(numrobot=3, collision_penalty=0.25, terminal_reward=1.5,
+                                      sensor_config={"num_lasers": 13, "range": 6.5}),
+                             lambda rs: bern(rs, 40, 40, 0.25), 8, 30),
+    "zero_cells": (base_cfg(numrobot=3, sensor_config={"num_lasers": 17, "range": 7}),
+                   lambda rs: tri(rs, 50, 50), 8, 30),
+    "square_r2": (base_cfg(numrobot=3, sensor_type="square_sensor", sensor_config={"range": 2}),
+                  lambda rs: tri(rs, 40, 40), 8, 30),
+    "square_r1_ego3": (base_cfg(numrobot=2, egoradius=3, sensor_type="square_sensor",
+                                sensor_config={"range": 1}),
+                       lambda rs: bern(rs, 30, 30, 0.2), 8, 30),
+    "single_square_tool": (base_cfg(numrobot=2, single_square_tool=1, sensor_type="square_sensor",
+                                    sensor_config={"range": 2}),
+                           lambda rs: bern(rs, 30, 30, 0.2), 8, 30),
+    "map_sharing_comm": (base_cfg(numrobot=4, comm_radius=7, allow_comm=1, map_sharing=1,
+                                  sensor_config={"num_lasers": 15, "range": 5}),
+                         lambda rs: bern(rs, 40, 40, 0.15), 8, 30),
+    "crowded_n12": (base_cfg(numrobot=12, collision_penalty=2,
+                             sensor_config={"num_lasers": 9, "range": 3}),
+                    lambda rs: bern(rs, 14, 14, 0.3), 8, 40),
+    "done_incr_small": (base_cfg(numrobot=2, done_thresh=0.2, done_incr=0.15, maxsteps=25,
+                                 sensor_config={"num_lasers": 11, "range": 4}),
+                        lambda rs: bern(rs, 16, 16, 0.1), 8, 40),
+    "ego0_range0": (base_cfg(numrobot=2, egoradius=0, sensor_config={"num_lasers": 5, "range": 0}),
+                    lambda rs: bern(rs, 12, 12, 0.1), 4, 20),
+    "n33_wide_window": (base_cfg(numrobot=33, sensor_config={"num_lasers": 7, "range": 3}),
+                        lambda rs: bern(rs, 30, 30, 0.1), 2, 10),
+}
+
+
+@pytest.mark.parametrize("name", sorted(BATCH_CASES))
+def test_batch_matches_oracle(torch_cuda, name):
+    import marlcov
+    torch = torch_cuda
+    cfg, maker, B, T = BATCH_CASES[name]
+    rs = np.random.RandomState(zlib.crc32(name.encode()))
+    grids = [maker(rs) for _ in range(B)]
+    N = cfg["numrobot"]
+    refs, pos = [], []
+    for b in range(B):
+        np.random.seed(1000 + b)
+        r = DecGridRLRef([grids[b]], cfg)
+        refs.append(r)
+        pos.append(np.stack([r._xinds, r._yinds], 1))
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False, want_adjacency=True)
+    obs, adj = env.reset(positions=np.stack(pos))
+    st = device_state(env)
+    obs_h = obs.cpu().numpy()
+    for b in range(B):
+        compare_env(st, b, refs[b], f"{name} reset env {b}")
+        np.testing.assert_array_equal(obs_h[b], refs[b].get_egocentric_observations(),
+                                      err_msg=f"{name} reset obs {b}")
+    for t in range(T):
+        acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+        acts[rs.rand(B, N) < 0.08] = rs.choice([4, 7, 200])
+        acts[rs.rand(B) < 0.05, 0] = 255
+        (obs, adj), rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h, adj_h = (obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(),
+                                       adj.cpu().numpy())
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"{name} t={t} env {b}"
+            assert abs(float(r) - rew_h[b]) <= REWARD_TOL, (tag, float(r), rew_h[b])
+            assert bool(d) == bool(done_h[b]), tag
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            np.testing.assert_array_equal(adj_h[b], refs[b]._adjacency_matrix, err_msg=tag + " adj")
+            compare_env(st, b, refs[b], tag)
+    env.check()
+
+
+# ---------------------------------------------------------------------------
+# 3. auto-reset: done envs restart in the same launch; the new episode equals
+#    the oracle's reset at the device-drawn start cells
+# ---------------------------------------------------------------------------
+def test_auto_reset_matches_oracle_reset(torch_cuda):
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=3, maxsteps=6, sensor_config={"num_lasers": 11, "range": 4})
+    rs = np.random.RandomState(7)
+    B = 16
+    grids = [bern(rs, 24, 24, 0.2) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=True, seed=123)
+    env.reset()
+    st = device_state(env)
+    refs = [oracle_from_device(st, b, cfg) for b in range(B)]
+    resets = 0
+    for t in range(20):
+        acts = rs.randint(0, 4, size=(B, 3)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), (t, b)
+            if d:
+                resets += 1
+                p = st["pos"][b]
+                assert len({tuple(q) for q in p}) == 3
+                for x, y in p:
+                    assert refs[b]._grid[x, y] >= 0
+                o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in p])
+                assert int(st["currstep"][b]) == 0
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=f"t={t} env {b}")
+            compare_env(st, b, refs[b], f"t={t} env {b}")
+    assert resets >= B  # maxsteps=6 over 20 steps: every env reset at least once
+    env.check()
+
+
+# ---------------------------------------------------------------------------
+# 4. BASELINE configs[1] at full size (4096 envs, 4 agents, 128x128, lidar
+#    21/10): size-independent invariants every step, plus oracle parity of a
+#    sample of envs re-built from device state mid-run
+# ---------------------------------------------------------------------------
+def popcount_rows(bits):
+    return bits.reshape(bits.shape[0], -1).sum(axis=1)
+
+
+def test_c2_full_size_invariants_and_sampled_parity(torch_cuda):
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=4)
+    B = 4096
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=128, length=128, prob_obst=0.1, seed=1000),
+                                   seed=5, auto_reset=True)
+    env.reset()
+    g = torch.Generator(device=env.device)
+    g.manual_seed(0)
+    for t in range(60):
+        acts = torch.randint(0, 4, (B, 4), dtype=torch.uint8, device=env.device, generator=g)
+        obs, rew, done = env.step(acts)
+    torch.cuda.synchronize()
+    env.check()
+    st = device_state(env)
+    # invariants (every env)
+    neg = st["neg"][st["env_grid"]]
+    assert not np.any(st["free"] & neg[:, None]), "free cell on an obstacle"
+    assert not np.any(st["obst"] & (1 - neg[:, None])), "obstacle mark on a free cell"
+    union = st["free"].max(axis=1)
+    np.testing.assert_array_equal(union, st["vis"])
+    np.testing.assert_array_equal(popcount_rows(st["free"]), st["free_cnt"])
+    np.testing.assert_array_equal(popcount_rows(st["vis"]), st["vis_cnt"])
+    p = st["pos"]
+    for b in range(0, B, 97):
+        assert len({tuple(q) for q in p[b]}) == 4
+    assert np.all(neg[np.arange(B)[:, None], p[..., 0], p[..., 1]] == 0)
+    # sampled parity: 24 envs re-built in the oracle, 8 more steps
+    sample = np.random.RandomState(3).choice(B, 24, replace=False)
+    refs = {b: oracle_from_device(st, b, cfg) for b in sample}
+    rs = np.random.RandomState(11)
+    for t in range(8):
+        acts = rs.randint(0, 4, size=(B, 4)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env)
+        for b in sample:
+            o, r, d = refs[b].step(acts[b].astype(np.int64))
+            assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), (t, b)
+            if d:  # auto-reset happened on the device: follow it
+                q = st["pos"][b]
+                o, _ = refs[b].reset(False, None, positions=[tuple(x) for x in q])
+            np.testing.assert_array_equal(obs_h[b], o)
+            compare_env(st, b, refs[b], f"c2 t={t} env {b}")
+
+
+def test_determinism_same_seed(torch_cuda):
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=4, maxsteps=20)
+    outs = []
+    for _ in range(2):
+        env = marlcov.BatchCoverageEnv(cfg, 256, gen=dict(width=64, length=64, prob_obst=0.1, seed=9),
+                                       seed=77, auto_reset=True)
+        env.reset()
+        g = torch.Generator(device=env.device)
+        g.manual_seed(1)
+        acc = []
+        for t in range(50):
+            acts = torch.randint(0, 4, (256, 4), dtype=torch.uint8, device=env.device, generator=g)
+            obs, rew, done = env.step(acts)
+            acc.append((obs.clone(), rew.clone(), done.clone()))
+        outs.append(acc)
+    for (o1, r1, d1), (o2, r2, d2) in zip(*outs):
+        assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2)

@@ -1,0 +1,144 @@
+"""CPU-only tests: the C-ABI library loads and exports every symbol of
+include/marlcov.h (no compute calls without a GPU), config validation, and
+the host-side logic of the package (action decoding, beam table, grids)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN_DIR, load_case
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import marlcov
+    from marlcov import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "marlcov.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mc_[a-z_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported_and_typed(lib):
+    from marlcov import _lib
+    names = header_functions()
+    assert len(names) >= 15
+    typed = {n for n, _, _ in _lib.SIGNATURES}
+    for n in names:
+        assert hasattr(lib, n), f"{n} not exported"
+        assert n in typed, f"{n} has no ctypes signature"
+
+
+def test_struct_layout_and_version(lib):
+    from marlcov import _lib
+    assert lib.mc_abi_version() == _lib.ABI_VERSION
+    assert lib.mc_struct_size(0) == ctypes.sizeof(_lib.McConfig)
+    assert lib.mc_struct_size(1) == ctypes.sizeof(_lib.McLayout)
+    assert lib.mc_struct_size(7) == -1
+
+
+def _cfg(**kw):
+    from marlcov import _lib
+    c = _lib.McConfig()
+    c.num_envs, c.num_agents, c.width, c.length, c.num_grids = 4, 4, 130, 130, 4
+    c.sensor_type, c.num_beams, c.lidar_range = _lib.SENSOR_LIDAR, 21, 10.0
+    c.egoradius, c.pad = 2, 2
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(num_envs=0), "num_envs"),
+    (dict(num_agents=65), "numrobot"),
+    (dict(num_agents=0), "numrobot"),
+    (dict(width=2), "padded grid"),
+    (dict(dist_reward=1), "ABI v1"),
+    (dict(dijkstra_input=1), "ABI v1"),
+    (dict(lidar_range=40.0), "range"),
+    (dict(egoradius=40, pad=40), "window"),
+    (dict(sensor_type=7), "sensor_type"),
+    (dict(pad=1), "pad"),
+])
+def test_create_rejects_bad_config(lib, bad, msg):
+    h = ctypes.c_void_p()
+    rc = lib.mc_create(ctypes.byref(_cfg(**bad)), 0, ctypes.byref(h))
+    assert rc == -1 and not h.value
+    assert msg in lib.mc_last_error().decode()
+
+
+def test_null_arguments_are_errors(lib):
+    assert lib.mc_create(None, 0, None) == -1
+    assert lib.mc_step(None, None, None, None, None, None, None) == -1
+    assert lib.mc_reset(None, None, None, None, None, None) == -1
+    assert lib.mc_query(None, None) == -1
+
+
+def test_decode_action_reference_semantics():
+    from marlcov.dec_grid_rl import decode_action
+    assert decode_action(None, 3) is None
+    assert decode_action(-1, 3) is None
+    assert decode_action(np.array([-1]), 1) is None
+    assert list(decode_action(27, 3)) == [3, 2, 1]             # base 4, robot 0 = LSD
+    assert list(decode_action(-2, 2)) == [2, 3]                # Python floor semantics
+    assert list(decode_action(np.int64(6), 2)) == [2, 1]
+    assert list(decode_action(2.5, 1)) == [4]                  # not 0..3 -> no-op
+    assert list(decode_action(np.array([7]), 1)) == [4]
+    assert list(decode_action([0, 3, 9], 3)) == [0, 3, 4]      # per-agent superset
+    assert list(decode_action(4 ** 16 - 1, 16)) == [3] * 16
+
+
+def test_beam_table_matches_golden_bits():
+    from marlcov import beam_angles, beam_increments
+    z = np.load(os.path.join(GOLDEN_DIR, "beam_tables.npz"))
+    for key in z.files:
+        tab = beam_increments(beam_angles(int(key[1:])))
+        np.testing.assert_array_equal(tab.view(np.uint64), z[key].view(np.uint64), err_msg=key)
+
+
+def test_gridload_handmade_matches_reference():
+    from marlcov import gridload
+    train, test = gridload(None)
+    case = load_case("square_r2_single_tool_handmade")
+    assert len(train) == 6 and len(test) == 3
+    np.testing.assert_array_equal(np.stack(train), case["train"].astype(np.float64))
+    np.testing.assert_array_equal(np.stack(test), case["test"].astype(np.float64))
+
+
+def test_gridgen_rng_sequence_and_split():
+    from marlcov import gridgen
+    np.random.seed(4)
+    tr, te = gridgen(dict(prob_obst=0.2, gridwidth=9, gridlen=7, numgrids=3))
+    np.random.seed(4)
+    exp = [np.random.choice(a=[1.0, -1.0], size=(9, 7), p=[0.8, 0.2]) for _ in range(3)]
+    assert te == [] and len(tr) == 3
+    for a, b in zip(tr, exp):
+        np.testing.assert_array_equal(a, b)
+    tr, te = gridgen(dict(prob_obst=0.2, gridwidth=9, gridlen=7, numgrids=1))
+    assert tr is te
+
+
+def test_grid_values_validated():
+    from marlcov.batch_env import grid_to_int8, pad_grid
+    g = pad_grid(np.array([[1.0, 0.0], [-1.0, 1.0]]))
+    assert g.shape == (4, 4) and g[0, 0] == -1
+    np.testing.assert_array_equal(grid_to_int8(g)[1:3, 1:3], [[1, 0], [-1, 1]])
+    with pytest.raises(ValueError):
+        grid_to_int8(np.array([[0.5]]))
+
+
+def test_bench_bytes_formula_matches_survey():
+    import bench
+    assert bench.algorithmic_bytes_per_env_step(1, 10, 2) == 893
+    assert bench.algorithmic_bytes_per_env_step(4, 10, 2) == 3476
+    assert bench.algorithmic_bytes_per_env_step(8, 20, 2) == 24280
