@@ -121,6 +121,9 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=8)
     ap.add_argument("--cpu-secs", type=float, default=2.5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--maxsteps", type=int, default=1000, help="episode length (auto-reset on done)")
+    ap.add_argument("--eager", action="store_true", help="plain launches + per-launch events (no hipGraph)")
+    ap.add_argument("--graph-chunk", type=int, default=100, help="steps captured per hipGraph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,7 +146,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True)
+    cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
+               maxsteps=args.maxsteps)
     N = c["numrobot"]
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
                                                     seed=1000 + rank, num_grids=B),
@@ -165,22 +169,53 @@ def main():
     torch.cuda.synchronize(dev)
     env.check()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    graphs = []
+    if not args.eager:
+        # K launches captured into hipGraphs (one per chunk of steps, each step
+        # reading its own action slice): the timed region replays them, so
+        # host launch overhead does not gate the GPU.  The kernel, its inputs
+        # and its work per step are unchanged.
+        chunk = max(1, min(args.graph_chunk, K))
+        for c0 in range(0, K, chunk):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                cs = torch.cuda.current_stream(dev).cuda_stream
+                for i in range(c0, min(K, c0 + chunk)):
+                    env.step_raw(actions[W + i].data_ptr(), rp, dp, op, cs)
+            graphs.append(g)
+        torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if args.eager:
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(K):
-        starts[i].record(stream)
-        env.step_raw(actions[W + i].data_ptr(), rp, dp, op, sp)
-        ends[i].record(stream)
+    ev0.record(stream)
+    if args.eager:
+        for i in range(K):
+            starts[i].record(stream)
+            env.step_raw(actions[W + i].data_ptr(), rp, dp, op, sp)
+            ends[i].record(stream)
+    else:
+        for g in graphs:
+            g.replay()
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / K
+    if args.eager:
+        kern_ms = sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K
+    else:
+        # HIP events on the launch stream around the replayed launches: the
+        # average includes the kernel boundaries, so it bounds the kernel
+        # duration from above (rocprofv3 in profiles/ gives the bare kernel)
+        kern_ms = ev0.elapsed_time(ev1) / K
     env.check()
 
     # scalar episode-return statistics: the only collective (outside timing)
@@ -212,10 +247,13 @@ def main():
         "dtype": "f64+u64",
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
-                   "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": 1000},
+                   "launch": "eager" if args.eager else "hipGraph replay",
+                   "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),
+                     "kernel_us_from": "per-launch HIP events" if args.eager else
+                                       "HIP events around the replayed launches / K (includes kernel boundaries)",
                      "alg_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }

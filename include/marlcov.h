@@ -170,6 +170,10 @@ int mc_set_state(void* env, int32_t field, const void* dev_src, int64_t bytes, v
 /* Synchronise `stream` and report (then clear) the device error word. */
 int mc_check(void* env, void* stream);
 
+/* Diagnostics: in a -DMC_STAMPS build, record per-phase s_memtime stamps of
+ * every env into dev_stamps uint64 [B][16]; MC_EINVAL in normal builds. */
+int mc_debug_stamps(void* env, uint64_t* dev_stamps);
+
 #ifdef __cplusplus
 }
 #endif

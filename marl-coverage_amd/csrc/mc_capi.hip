@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -46,11 +47,15 @@ int fail(int code, const char* fmt, ...) {
 
 struct Env {
   mc_config cfg;
+  double range = 0.0;
   mc_layout lay;
   mc::State s;
   int device = 0;
   int nt = 128;
   bool beams_set = false;
+  void* beams_buf = nullptr;  // mc::Beam [beam_count]
+  void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
+  int beam_count = 0;
   bool grids_set = false;
   std::vector<void*> allocs;
 };
@@ -92,13 +97,15 @@ int dev_alloc(Env* E, void** p, size_t bytes) {
 }
 
 int env_threads(const mc::State& s) {
-  // enough lanes for the widest phase: beams (lidar), staged rows, union slots
-  int work = s.N * s.Wwin * 2;
-  if (s.sensor == MC_SENSOR_LIDAR) work = work > s.N * s.nbeams ? work : s.N * s.nbeams;
-  if (work <= 64) return 64;
-  if (work <= 128) return 128;
-  if (work <= 1024) return 256;
-  return 512;
+  // every lane stages at most kMaxItemsPerLane (agent, row) items; beyond
+  // that, prefer one wave per env (no cross-wave barriers) unless the beam
+  // march would need more than ~8 sequential rounds per lane
+  const int items = s.N * s.We;
+  int nt = 64;
+  while (nt < 1024 && items > mc::kMaxItemsPerLane * nt) nt *= 2;
+  if (s.sensor == MC_SENSOR_LIDAR)
+    while (nt < 256 && s.N * s.nbeams > 8 * nt) nt *= 2;
+  return nt;
 }
 
 Env* as_env(void* p) { return static_cast<Env*>(p); }
@@ -140,6 +147,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   if (c.dist_reward || c.dijkstra_input)
     return fail(MC_EINVAL, "dist_reward / dijkstra_input layers are not in ABI v1");
   if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
+  if (c.maxsteps < 0) return fail(MC_EINVAL, "maxsteps must be >= 0");
 
   int hs = 0;
   if (c.sensor_type == MC_SENSOR_LIDAR) {
@@ -152,11 +160,15 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     hs = c.square_radius;
   }
   const int H = hs > c.egoradius ? hs : c.egoradius;
-  if (2 * H + 1 > 63)
-    return fail(MC_EINVAL, "window 2H+1 = %d exceeds 63 (range/egoradius too large)", 2 * H + 1);
+  if (2 * H + 3 > 63)
+    return fail(MC_EINVAL, "staged window 2H+3 = %d exceeds 63 (range/egoradius too large)", 2 * H + 3);
+  if ((int64_t)c.num_agents * (2 * H + 3) > 2 * 1024)
+    return fail(MC_EINVAL, "numrobot * (2H+3) = %d staged rows exceeds 2048",
+                c.num_agents * (2 * H + 3));
 
   Env* E = new Env();
   E->cfg = c;
+  E->range = c.lidar_range;
   E->device = hip_device;
   mc::State& s = E->s;
   s.B = c.num_envs;
@@ -166,14 +178,17 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.nw = (c.length + 63) / 64;
   s.G = c.num_grids;
   s.H = H;
-  s.Wwin = 2 * H + 1;
+  s.We = 2 * H + 3;
+  s.mg_We = mc::magic_div((uint32_t)s.We);
   s.ego = c.egoradius;
   s.E = 2 * c.egoradius + 1;
   s.Lc = 3;
+  s.mg_LcE = mc::magic_div((uint32_t)(s.Lc * s.E));
+  s.mg_E = mc::magic_div((uint32_t)s.E);
   s.sensor = c.sensor_type;
   s.nbeams = c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0;
+  s.mg_nb = mc::magic_div((uint32_t)(s.nbeams > 0 ? s.nbeams : 1));
   s.sq_r = c.square_radius;
-  s.range = c.lidar_range;
   s.pen = c.collision_penalty;
   s.term = c.terminal_reward;
   s.dincr = c.done_incr;
@@ -201,11 +216,9 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   } while (0)
   uint64_t *gneg = nullptr, *gpos = nullptr;
   int32_t* nfree = nullptr;
-  double* beams = nullptr;
   ALLOC(gneg, uint64_t, G * mw);
   ALLOC(gpos, uint64_t, G * mw);
   ALLOC(nfree, int32_t, G);
-  ALLOC(beams, double, (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 3);
   ALLOC(s.env_grid, int32_t, B);
   ALLOC(s.pos, int32_t, B * N * 2);
   ALLOC(s.moved, uint64_t, B);
@@ -222,7 +235,6 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.grid_neg = gneg;
   s.grid_pos = gpos;
   s.numfree = nfree;
-  s.beams = beams;
   if (rc != MC_OK) {
     std::string msg = g_err;
     mc_destroy(E);
@@ -239,6 +251,10 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     }
   }
   E->nt = env_threads(s);
+  if (const char* ov = getenv("MARLCOV_NT")) {  // tuning override (64..1024)
+    const int v = atoi(ov);
+    if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) E->nt = v > E->nt ? v : E->nt;
+  }
   mc_layout& L = E->lay;
   L.words_per_row = s.nw;
   L.window_half = s.H;
@@ -257,6 +273,8 @@ void mc_destroy(void* env) {
   if (!E) return;
   (void)hipSetDevice(E->device);
   for (void* p : E->allocs) (void)hipFree(p);
+  if (E->beams_buf) (void)hipFree(E->beams_buf);
+  if (E->bits_buf) (void)hipFree(E->bits_buf);
   delete E;
 }
 
@@ -271,27 +289,74 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   if (!E || !host_table) return fail(MC_EINVAL, "mc_set_beam_table: null argument");
   if (E->s.sensor != MC_SENSOR_LIDAR) return fail(MC_EINVAL, "beam table on a non-lidar env");
   if (num_beams < 1) return fail(MC_EINVAL, "beam table needs >= 1 beam");
+  const int cmax = E->s.Wp > E->s.Lp ? E->s.Wp : E->s.Lp;
+  std::vector<mc::Beam> bt(num_beams);
+  std::vector<uint64_t> bits((size_t)num_beams * cmax, 0);
   for (int b = 0; b < num_beams; ++b) {
     const double xi = host_table[3 * b], yi = host_table[3 * b + 1], di = host_table[3 * b + 2];
-    if (!(fabs(xi) <= 1.0 && fabs(yi) <= 1.0 && di >= 1.0 && (fabs(xi) == 1.0 || fabs(yi) == 1.0)))
-      return fail(MC_EINVAL, "beam %d is not a normalised lidar.py increment (%g, %g, %g)", b, xi,
-                  yi, di);
+    mc::Beam& o = bt[b];
+    double minor;
+    // lidar.py:43-45 normalises by max(|xinc|, |yinc|): one of them is +-1
+    if (fabs(xi) == 1.0 && fabs(yi) <= 1.0) {
+      o.axis = 0; o.sign = xi > 0 ? 1 : -1; minor = yi;
+    } else if (fabs(yi) == 1.0 && fabs(xi) <= 1.0) {
+      o.axis = 1; o.sign = yi > 0 ? 1 : -1; minor = xi;
+    } else {
+      return fail(MC_EINVAL, "beam %d is not a normalised lidar.py increment (%g, %g)", b, xi, yi);
+    }
+    o.msign = minor > 0 ? 1 : (minor < 0 ? -1 : 0);
+    o.pad_ = 0;
+    if (!(di >= 1.0)) return fail(MC_EINVAL, "beam %d distinc %g < 1", b, di);
+    // currdist = 0; while currdist < range: currdist += distinc  (lidar.py:49-56)
+    double dist = 0.0;
+    int K = 0;
+    while (dist < E->range && K <= 64) { dist += di; ++K; }
+    if (K > E->s.H)
+      return fail(MC_EINVAL, "beam %d takes %d steps > window half-width %d", b, K, E->s.H);
+    o.K = K;
+    // the reference's minor-coordinate chain (currx/curry += inc, int() of it)
+    // from every integer start; valid starts are the padded-grid interior
+    const int cm = o.axis == 0 ? E->s.Lp : E->s.Wp;
+    for (int c0 = 0; c0 < cm; ++c0) {
+      double m = (double)c0;
+      int cell = c0;
+      uint64_t w = 0;
+      for (int k = 0; k < K; ++k) {
+        m += minor;
+        const int next = (int)m;  // trunc toward zero, as Python int()
+        const int d = next - cell;
+        if (d != 0 && d != o.msign) {
+          if (m >= 0.0)  // negative coordinates lie outside the grid: unused
+            return fail(MC_EINVAL, "beam %d start %d: minor step %d at k=%d", b, c0, d, k);
+        }
+        if (d != 0) w |= 1ull << k;
+        cell = next;
+      }
+      bits[(size_t)b * cmax + c0] = w;
+    }
   }
   HIP_TRY(hipSetDevice(E->device));
-  if (num_beams != E->s.nbeams) {
+  if (num_beams != E->beam_count || !E->beams_buf) {
     // the reference lets callers swap _thetalist after construction
-    // (even beam counts); re-size the device table
+    // (even beam counts): (re-)size the device tables
     HIP_TRY(hipDeviceSynchronize());
-    void* nb = nullptr;
-    HIP_TRY(hipMalloc(&nb, (size_t)num_beams * 3 * sizeof(double)));
-    for (auto& p : E->allocs)
-      if (p == (void*)E->s.beams) { (void)hipFree(p); p = nb; }
-    E->s.beams = (const double*)nb;
+    if (E->beams_buf) (void)hipFree(E->beams_buf);
+    if (E->bits_buf) (void)hipFree(E->bits_buf);
+    E->beams_buf = E->bits_buf = nullptr;
+    HIP_TRY(hipMalloc(&E->beams_buf, (size_t)num_beams * sizeof(mc::Beam)));
+    HIP_TRY(hipMalloc(&E->bits_buf, bits.size() * sizeof(uint64_t)));
+    E->beam_count = num_beams;
+    E->s.beams = (const mc::Beam*)E->beams_buf;
+    E->s.beam_bits = (const uint64_t*)E->bits_buf;
+    E->s.bcmax = cmax;
     E->s.nbeams = num_beams;
+    E->s.mg_nb = mc::magic_div((uint32_t)num_beams);
     E->cfg.num_beams = num_beams;
     E->nt = env_threads(E->s);
   }
-  HIP_TRY(hipMemcpy((void*)E->s.beams, host_table, (size_t)num_beams * 3 * sizeof(double),
+  HIP_TRY(hipMemcpy((void*)E->s.beams, bt.data(), (size_t)num_beams * sizeof(mc::Beam),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy((void*)E->s.beam_bits, bits.data(), bits.size() * sizeof(uint64_t),
                     hipMemcpyHostToDevice));
   E->beams_set = true;
   return MC_OK;
@@ -405,6 +470,19 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (f == MC_FIELD_GRID_NEG || f == MC_FIELD_GRID_POS || f == MC_FIELD_NUMFREE) E->grids_set = true;
   return MC_OK;
+}
+
+// Diagnostic builds only: point the kernels at a [B][16] u64 stamp buffer.
+int mc_debug_stamps(void* env, uint64_t* dev_stamps) {
+  Env* E = as_env(env);
+  if (!E) return fail(MC_EINVAL, "mc_debug_stamps: null env");
+#ifdef MC_STAMPS
+  E->s.stamps = dev_stamps;
+  return MC_OK;
+#else
+  (void)dev_stamps;
+  return fail(MC_EINVAL, "not a -DMC_STAMPS build");
+#endif
 }
 
 int mc_check(void* env, void* stream) {

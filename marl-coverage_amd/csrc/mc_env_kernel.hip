@@ -1,0 +1,792 @@
+// mc_env_kernel.hip — the step / reset kernel of the batched coverage env.
+//
+// Hot path restated from ExistentialRobotics/MARL-Coverage
+//   Environments/dec_grid_rl.py  DecGridRL.step :91-169, reset :449-531
+//   Environments/Sensors/lidar.py LidarSensor.getMeasurement :16-65
+//   Environments/Sensors/squaresensor.py SquareSensor.getMeasurement :15-37
+//
+// One workgroup = one env (one wave for the BASELINE configs).  Per step:
+//   round trip 1  positions, actions, per-env scalars
+//   round trip 2  for every agent the (2H+3)-row "extended window" around its
+//                 pre-move cell: grid neg/pos bits, its free/obst mask words,
+//                 the union (visited) words — 2 u64 per row and plane.  The
+//                 +1 margin covers every post-move window, so the sequential
+//                 moves, the beam march and the merge need no further loads.
+//   LDS compute   moves (wave-serial in robot order, readlane/ballot), lidar or
+//                 square sensing as LDS bit tests + ds_or_b64 marks (two beams
+//                 interleaved per lane), merge with popcounts
+//   stores        changed mask words (plain stores: one writer per word),
+//                 newly covered union bits (global_atomic_or: agents' windows
+//                 overlap), positions, counters, reward, done, obs
+// All float64 arithmetic is the reference's: the minor beam coordinate is a
+// sequential `+=` from the robot cell (adds only: nothing to contract into an
+// FMA); the major coordinate moves by exactly +-1 (|inc| == 1 after the
+// normalisation of lidar.py:43-45); rewards are assembled in reference order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mc_device.h"
+
+namespace mc {
+
+#ifdef MC_STAMPS
+#define STAMP(k)                                                                       \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    uint64_t _t;                                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
+    if (threadIdx.x == 0 && s.stamps) s.stamps[(size_t)blockIdx.x * 16 + (k)] = _t;    \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
+constexpr int KI = kMaxItemsPerLane;
+
+// n / d via the magic reciprocal of mc_internal.h (magic == 0 encodes d == 1)
+__device__ __forceinline__ int udiv(int n, uint32_t magic) {
+  return magic ? (int)__umulhi((uint32_t)n, magic) : n;
+}
+
+__device__ __forceinline__ int rdlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+struct Scal {
+  double pen;          // move penalties, accumulated in robot order
+  double done_thresh;
+  uint64_t moved;      // robots present in the reference's _robot_pad
+  uint32_t cnt_free;   // newly set bits over all agents' free maps
+  uint32_t cnt_vis;    // newly covered union cells (the obs reward)
+  uint32_t free_old, vis_old;
+  int32_t grid, numfree, currstep;
+  uint32_t ep;
+  int32_t do_reset;
+  int32_t pad_;
+};
+static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
+
+struct Lds {
+  uint64_t *neg, *pos, *fold, *oold, *fp, *op;
+  Beam* beams;
+  int32_t *x0, *y0, *x, *y;
+  Scal* sc;
+  uint8_t* act;
+  uint8_t* obsrow;  // [N*Lc*E] E-bit crop rows
+};
+
+__device__ __forceinline__ Lds carve(char* smem, const State& s) {
+  Lds L;
+  const int items = s.N * s.We;
+  uint64_t* p = reinterpret_cast<uint64_t*>(smem);
+  L.neg = p;
+  L.pos = p + items;
+  L.fold = p + 2 * items;
+  L.oold = p + 3 * items;
+  L.fp = p + 4 * items;
+  L.op = p + 5 * items;
+  char* q = reinterpret_cast<char*>(p + 6 * items);
+  L.beams = reinterpret_cast<Beam*>(q);
+  q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
+  L.x0 = reinterpret_cast<int32_t*>(q);
+  L.y0 = L.x0 + s.N;
+  L.x = L.y0 + s.N;
+  L.y = L.x + s.N;
+  q += (size_t)s.N * 16;
+  L.sc = reinterpret_cast<Scal*>(q);
+  q += 64;
+  L.act = reinterpret_cast<uint8_t*>(q);
+  q += ((size_t)s.N + 15) & ~(size_t)15;
+  L.obsrow = reinterpret_cast<uint8_t*>(q);
+  return L;
+}
+
+// Per lane: agent (lane % 64)'s cells in registers, so loops over agents use
+// v_readlane (SGPR) instead of LDS round trips.  N <= 64.
+struct Agents {
+  int x0, y0;  // pre-move (extended-window origin basis)
+  int x, y;    // post-move
+};
+
+__device__ __forceinline__ Agents load_agents(const State& s, const Lds& L) {
+  const int j = threadIdx.x & 63;
+  Agents A;
+  const bool ok = j < s.N;
+  A.x0 = ok ? L.x0[j] : 0;
+  A.y0 = ok ? L.y0[j] : 0;
+  A.x = ok ? L.x[j] : 0;
+  A.y = ok ? L.y[j] : 0;
+  return A;
+}
+
+// staged (agent, row) items of this lane; raw HBM words stay in registers
+// from stage to store
+struct Items {
+  int a[KI], gx[KI], oy[KI];
+  uint64_t f0[KI], f1[KI], o0[KI], o1[KI], u0[KI], u1[KI];
+  uint64_t nf[KI], no[KI], nu[KI];
+};
+
+__device__ __forceinline__ bool row_in(const State& s, int gx) { return gx >= 0 && gx < s.Wp; }
+__device__ __forceinline__ bool word0_in(const State& s, int gx, int oy) {
+  const int w0 = oy >> 6;
+  return row_in(s, gx) && w0 >= 0 && w0 < s.nw;
+}
+__device__ __forceinline__ bool word1_in(const State& s, int gx, int oy) {
+  const int w1 = (oy >> 6) + 1;
+  return row_in(s, gx) && w1 >= 0 && w1 < s.nw && (oy & 63) != 0;
+}
+
+// --------------------------------------------------------------------------
+// stage: one round trip for every staged row (masks known zero after reset)
+// --------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void stage(const State& s, const Lds& L, int e, bool load_masks, Items& I) {
+  const int items = s.N * s.We;
+  const size_t mw = (size_t)s.Wp * s.nw;
+  const int g = L.sc->grid;
+  const uint64_t* gn = s.grid_neg + (size_t)g * mw;
+  const uint64_t* gp = s.grid_pos + (size_t)g * mw;
+  const uint64_t wmask = low_mask(s.We);
+  const bool square = s.sensor == 1;
+  uint64_t n0[KI], n1[KI], p0[KI], p1[KI];
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = threadIdx.x + k * NT;
+    n0[k] = n1[k] = ~0ull;
+    p0[k] = p1[k] = 0;
+    I.f0[k] = I.f1[k] = I.o0[k] = I.o1[k] = I.u0[k] = I.u1[k] = 0;
+    I.a[k] = 0;
+    I.gx[k] = -1;
+    I.oy[k] = 0;
+    if (idx < items) {
+      const int a = udiv(idx, s.mg_We);
+      const int r = idx - a * s.We;
+      const int gx = L.x0[a] - s.H - 1 + r;
+      const int oy = L.y0[a] - s.H - 1;
+      I.a[k] = a;
+      I.gx[k] = gx;
+      I.oy[k] = oy;
+      const int w0 = oy >> 6;
+      const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
+      const size_t rb = (size_t)(row_in(s, gx) ? gx : 0) * s.nw;
+      const size_t fb = ((size_t)e * s.N + a) * mw + rb;
+      const size_t vb = (size_t)e * mw + rb;
+      if (in0) {
+        n0[k] = gn[rb + w0];
+        if (square) p0[k] = gp[rb + w0];
+        if (load_masks) {
+          I.f0[k] = s.freem[fb + w0];
+          I.o0[k] = s.obstm[fb + w0];
+          I.u0[k] = s.vis[vb + w0];
+        }
+      }
+      if (in1) {
+        n1[k] = gn[rb + w0 + 1];
+        if (square) p1[k] = gp[rb + w0 + 1];
+        if (load_masks) {
+          I.f1[k] = s.freem[fb + w0 + 1];
+          I.o1[k] = s.obstm[fb + w0 + 1];
+          I.u1[k] = s.vis[vb + w0 + 1];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = threadIdx.x + k * NT;
+    if (idx < items) {
+      const int off = I.oy[k] & 63;
+      L.neg[idx] = funnel(n0[k], n1[k], off) & wmask;
+      L.pos[idx] = funnel(p0[k], p1[k], off) & wmask;
+      L.fold[idx] = funnel(I.f0[k], I.f1[k], off) & wmask;
+      L.oold[idx] = funnel(I.o0[k], I.o1[k], off) & wmask;
+      L.fp[idx] = 0;
+      L.op[idx] = 0;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// moves: updateRobotPos in robot order (dec_grid_rl.py:128-145, :171-204).
+// Wave 0, lane i = robot i.  Occupancy is the live position set: a robot may
+// enter a cell vacated earlier in this step and is blocked by a higher-index
+// robot that has not moved yet (:186,190-199,310).  The grid test at the
+// target reads the staged extended window (1 outside the grid = isInBounds).
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void moves(const State& s, const Lds& L, double pen_unit) {
+  const int lane = threadIdx.x;
+  const int N = s.N;
+  const bool live = lane < N;
+  int x = live ? L.x0[lane] : INT32_MIN / 2;
+  int y = live ? L.y0[lane] : INT32_MIN / 2;
+  const int act = live ? (int)L.act[lane] : 255;
+  const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+  int gblk = 1;
+  if (live && act < 4) {
+    const uint64_t row = L.neg[lane * s.We + s.H + 1 + dx];
+    gblk = (int)((row >> (s.H + 1 + dy)) & 1ull);
+  }
+  const int tx = x + dx, ty = y + dy;
+  double pen = 0.0;
+  uint64_t moved = L.sc->moved;
+  for (int i = 0; i < N; ++i) {
+    if (rdlane(act, i) > 3) continue;  // not 0..3: no updateRobotPos call, no penalty
+    const int txi = rdlane(tx, i), tyi = rdlane(ty, i);
+    const bool occ = __ballot(live && x == txi && y == tyi) != 0ull;
+    if (!rdlane(gblk, i) && !occ) {
+      if (lane == i) { x = txi; y = tyi; }
+      moved |= 1ull << i;
+    } else {
+      pen += pen_unit;  // reward += -collision_penalty (:203)
+    }
+  }
+  if (live) { L.x[lane] = x; L.y[lane] = y; }
+  if (lane == 0) { L.sc->pen = pen; L.sc->moved = moved; }
+}
+
+// --------------------------------------------------------------------------
+// lidar march (lidar.py:34-63), integer form.  The major coordinate moves
+// exactly +-1 per step; the minor cell moves by msign at the steps flagged in
+// the host-built beam_bits word for this (beam, start coordinate), which
+// encodes the reference's float64 `+=` chain bit-exactly (mc_internal.h).
+// Two beams per lane advance in lock step; the body is branch-free: both
+// neg-row reads are issued before either mark, and a mark is one ds_or_b64
+// into fp (free) or op (obstacle, ends the beam), with a zero operand once
+// the beam is over.
+// --------------------------------------------------------------------------
+struct Ray {
+  uint64_t bits;
+  int r, c, dr, dc, mr, mc, K, base;
+  bool live;
+};
+
+__device__ __forceinline__ Ray ray_init(const State& s, const Lds& L, int idx) {
+  Ray R;
+  R.live = idx < s.N * s.nbeams;
+  const int a = R.live ? udiv(idx, s.mg_nb) : 0;
+  const int b = R.live ? idx - a * s.nbeams : 0;
+  const Beam bm = L.beams[b];
+  const int xa = L.x[a], ya = L.y[a];
+  R.r = xa - (L.x0[a] - s.H - 1);
+  R.c = ya - (L.y0[a] - s.H - 1);
+  const bool ax = bm.axis == 0;
+  R.dr = ax ? bm.sign : 0;
+  R.dc = ax ? 0 : bm.sign;
+  R.mr = ax ? 0 : bm.msign;
+  R.mc = ax ? bm.msign : 0;
+  R.K = R.live ? bm.K : -1;
+  R.base = a * s.We;
+#if defined(MC_ABL) && MC_ABL == 2
+  R.bits = 0x5555555555555555ull;  // timing ablation only: no table load
+#else
+  R.bits = R.live ? s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0ull;
+#endif
+  return R;
+}
+
+// cell of step k: window row/col (clamped to 0 when outside the window, with
+// `bad` recording a beam that left it) — independent of earlier hits, so the
+// LDS reads of several steps can be in flight together
+__device__ __forceinline__ void ray_cell(const State& s, const Ray& R, int& r, int& c, bool& inwin) {
+  inwin = (unsigned)R.r < (unsigned)s.We && (unsigned)R.c < (unsigned)s.We;
+  r = inwin ? R.r : 0;
+  c = inwin ? R.c : 0;
+}
+
+__device__ __forceinline__ void ray_advance(Ray& R, int k) {
+  const int mv = (int)((R.bits >> k) & 1ull);
+  R.r += R.dr + mv * R.mr;
+  R.c += R.dc + mv * R.mc;
+}
+
+// mark step k (free, or obstacle = end of beam); skip the OR when the free
+// bit is already set (most cells near the robot are hit by many beams)
+__device__ __forceinline__ void ray_mark(const Lds& L, Ray& R, int k, bool inwin, int r, int c,
+                                         uint64_t nrow, uint64_t frow, bool& bad) {
+  const bool run = R.live && k <= R.K;
+  bad |= run && !inwin;
+  const bool on = run && inwin;
+  const uint64_t bit = 1ull << c;
+  const bool hit = (nrow & bit) != 0ull;  // oc[int(cx), int(cy)] < 0
+  if (on && (hit || !(frow & bit))) {
+    uint64_t* dst = (hit ? L.op : L.fp) + R.base + r;
+    atomicOr((unsigned long long*)dst, bit);
+  }
+  R.live = on && !hit;
+}
+
+template <int NT>
+__device__ __forceinline__ void sense(const State& s, const Lds& L) {
+  const int N = s.N, We = s.We, H = s.H;
+  if (s.sensor == 0) {
+#if defined(MC_ABL) && MC_ABL == 3
+    return;  // timing ablation only: no march
+#endif
+    // step 0 of every beam is the robot's own (free) cell: mark it once
+    for (int a = threadIdx.x; a < N; a += NT) {
+      const int r0 = L.x[a] - (L.x0[a] - H - 1), c0 = L.y[a] - (L.y0[a] - H - 1);
+      if ((unsigned)r0 < (unsigned)We && (unsigned)c0 < (unsigned)We)
+        atomicOr((unsigned long long*)&L.fp[a * We + r0], 1ull << c0);
+    }
+    const int total = N * s.nbeams;
+    bool bad = false;
+    for (int base = threadIdx.x; base < total; base += 2 * NT) {
+      Ray q0 = ray_init(s, L, base), q1 = ray_init(s, L, base + NT);
+      ray_advance(q0, 0);
+      ray_advance(q1, 0);
+      const int kmax = max(q0.K, q1.K);
+      for (int k = 1; k <= kmax; k += 2) {
+        // cells of steps k, k+1 for both rays; all eight row reads in flight
+        int ra0, ca0, ra1, ca1, rb0, cb0, rb1, cb1;
+        bool ia0, ia1, ib0, ib1;
+        ray_cell(s, q0, ra0, ca0, ia0);
+        ray_cell(s, q1, ra1, ca1, ia1);
+        Ray n0 = q0, n1 = q1;
+        ray_advance(n0, k);
+        ray_advance(n1, k);
+        ray_cell(s, n0, rb0, cb0, ib0);
+        ray_cell(s, n1, rb1, cb1, ib1);
+        const uint64_t na0 = L.neg[q0.base + ra0], fa0 = L.fp[q0.base + ra0];
+        const uint64_t na1 = L.neg[q1.base + ra1], fa1 = L.fp[q1.base + ra1];
+        const uint64_t nb0 = L.neg[q0.base + rb0], fb0 = L.fp[q0.base + rb0];
+        const uint64_t nb1 = L.neg[q1.base + rb1], fb1 = L.fp[q1.base + rb1];
+        ray_mark(L, q0, k, ia0, ra0, ca0, na0, fa0, bad);
+        ray_mark(L, q1, k, ia1, ra1, ca1, na1, fa1, bad);
+        n0.live = q0.live;
+        n1.live = q1.live;
+        ray_mark(L, n0, k + 1, ib0, rb0, cb0, nb0, fb0, bad);
+        ray_mark(L, n1, k + 1, ib1, rb1, cb1, nb1, fb1, bad);
+        ray_advance(n0, k + 1);
+        ray_advance(n1, k + 1);
+        q0 = n0;
+        q1 = n1;
+      }
+    }
+    if (bad) atomicOr(s.err, ERR_WINDOW);
+  } else {
+    // window [x-r, x+r] x [y-r, y+r] clamped to the padded grid; the
+    // reference overwrites it with clip(g,0,1) / clip(-g,0,1), which on a
+    // static grid is an OR (every free bit comes from clip(g,0,1)).
+    const int rr = s.sq_r;
+    for (int idx = threadIdx.x; idx < N * We; idx += NT) {
+      const int a = udiv(idx, s.mg_We), r = idx - a * We;
+      const int ox = L.x0[a] - H - 1, oy = L.y0[a] - H - 1;
+      const int gx = ox + r, xa = L.x[a], ya = L.y[a];
+      uint64_t f = 0, o = 0;
+      if (gx >= xa - rr && gx <= xa + rr && gx >= 0 && gx < s.Wp) {
+        int c0 = ya - rr - oy, c1 = ya + rr - oy;      // extended-window columns
+        if (c0 < -oy) c0 = -oy;                          // grid column 0
+        if (c1 > s.Lp - 1 - oy) c1 = s.Lp - 1 - oy;      // grid column Lp-1
+        if (c1 >= c0) {
+          const uint64_t cm = low_mask(c1 + 1) & ~low_mask(c0);
+          f = L.pos[idx] & cm;
+          o = L.neg[idx] & cm;
+        }
+      }
+      L.fp[idx] = f;
+      L.op[idx] = o;
+    }
+  }
+}
+
+// single_square_tool: only the robot's own cell becomes free (:233-234)
+template <int NT>
+__device__ __forceinline__ void single_tool(const State& s, const Lds& L) {
+  for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
+    const int a = udiv(idx, s.mg_We), r = idx - a * s.We;
+    const int ox = L.x0[a] - s.H - 1, oy = L.y0[a] - s.H - 1;
+    L.fp[idx] = (ox + r == L.x[a]) ? (1ull << (L.y[a] - oy)) : 0ull;
+  }
+}
+
+// --------------------------------------------------------------------------
+// merge (dec_grid_rl.py:232-256): newly set free bits per agent, and the
+// union delta = cells some agent marked this step that were not yet visited,
+// each counted at the lowest-index agent that marked it.
+// --------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void merge(const State& s, const Lds& L, Items& I, const Agents& A) {
+  const int items = s.N * s.We;
+  const uint64_t wmask = low_mask(s.We);
+  uint32_t cf = 0, cv = 0;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = threadIdx.x + k * NT;
+    I.nf[k] = I.no[k] = I.nu[k] = 0;
+    if (idx < items) {
+      const uint64_t fp = L.fp[idx], op = L.op[idx];
+      I.nf[k] = fp & ~L.fold[idx];
+      I.no[k] = op & ~L.oold[idx];
+      cf += __popcll(I.nf[k]);
+      const int a = I.a[k], gx = I.gx[k], oy = I.oy[k];
+      uint64_t cand = fp & ~(funnel(I.u0[k], I.u1[k], oy & 63) & wmask);
+      if (cand) {
+        for (int b = 0; b < s.N; ++b) {  // marks of lower-index agents at these cells
+          const int xb = rdlane(A.x0, b), yb = rdlane(A.y0, b);
+          const int rb = gx - (xb - s.H - 1);
+          const int d = (yb - s.H - 1) - oy;  // column shift b -> a (|d| < We to overlap)
+          if (b < a && (unsigned)rb < (unsigned)s.We && d > -s.We && d < s.We) {
+            const uint64_t pb = L.fp[b * s.We + rb];
+            cand &= ~(d >= 0 ? (pb << d) : (pb >> -d));
+          }
+        }
+      }
+      I.nu[k] = cand;
+      cv += __popcll(cand);
+    }
+  }
+  if (cf) atomicAdd(&L.sc->cnt_free, cf);
+  if (cv) atomicAdd(&L.sc->cnt_vis, cv);
+}
+
+// after merge: fold |= fp (obs crops read the post-step maps)
+template <int NT>
+__device__ __forceinline__ void fold_marks(const State& s, const Lds& L) {
+  for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
+    L.fold[idx] |= L.fp[idx];
+    L.oold[idx] |= L.op[idx];
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_words(const State& s, int e, const Items& I) {
+  const int items = s.N * s.We;
+  const size_t mw = (size_t)s.Wp * s.nw;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = threadIdx.x + k * NT;
+    if (idx >= items) continue;
+    const int gx = I.gx[k], oy = I.oy[k];
+    if (!row_in(s, gx)) continue;
+    const int w0 = oy >> 6, off = oy & 63;
+    const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
+    const size_t rb = (size_t)gx * s.nw;
+    const size_t fb = ((size_t)e * s.N + I.a[k]) * mw + rb;
+    const uint64_t nf = I.nf[k], no = I.no[k], nu = I.nu[k];
+    if (nf) {
+      if (in0) s.freem[fb + w0] = I.f0[k] | (nf << off);
+      if (in1) s.freem[fb + w0 + 1] = I.f1[k] | (nf >> (64 - off));
+    }
+    if (no) {
+      if (in0) s.obstm[fb + w0] = I.o0[k] | (no << off);
+      if (in1) s.obstm[fb + w0 + 1] = I.o1[k] | (no >> (64 - off));
+    }
+    if (nu) {  // agents' windows overlap: several lanes may add bits to one word
+      unsigned long long* v = (unsigned long long*)(s.vis + (size_t)e * mw + rb);
+      if (in0 && (nu << off)) atomicOr(v + w0, nu << off);
+      if (in1 && (nu >> (64 - off))) atomicOr(v + w0 + 1, nu >> (64 - off));
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// reset (dec_grid_rl.py:449-531) of env e inside the launch: grid pick, start
+// cells (injected, or Philox rejection draw with the reference's acceptance
+// rule, :491-502), zeroed maps, initial observe() (reward discarded, :524).
+// --------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void reset_env(const State& s, const Lds& L, int e, const int32_t* inj_pos) {
+  const int N = s.N;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const uint32_t ep = s.episode[e] + 1u;
+    s.episode[e] = ep;
+    L.sc->ep = ep;
+    if (s.grid_mode == 1) {
+      const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, (uint32_t)e, ep, 0x67726964u));
+      const int g = (int)bounded(r.x, (uint32_t)s.G);
+      L.sc->grid = g;
+      s.env_grid[e] = g;
+    }
+    L.sc->moved = 0;
+    L.sc->cnt_free = 0;
+    L.sc->cnt_vis = 0;
+  }
+  __syncthreads();
+  const uint32_t ep = L.sc->ep;
+  const int g = L.sc->grid;
+  const size_t mw = (size_t)s.Wp * s.nw;
+  {  // zero this env's maps (:505-514)
+    uint64_t* f = s.freem + (size_t)e * N * mw;
+    uint64_t* o = s.obstm + (size_t)e * N * mw;
+    for (size_t i = tid; i < (size_t)N * mw; i += NT) { f[i] = 0; o[i] = 0; }
+    uint64_t* v = s.vis + (size_t)e * mw;
+    for (size_t i = tid; i < mw; i += NT) v[i] = 0;
+  }
+  if (inj_pos != nullptr) {
+    if (tid < N) {
+      const int x = inj_pos[((size_t)e * N + tid) * 2];
+      const int y = inj_pos[((size_t)e * N + tid) * 2 + 1];
+      bool bad = grid_blocked(s, g, x, y);
+      for (int j = 0; j < tid; ++j)
+        bad |= (inj_pos[((size_t)e * N + j) * 2] == x && inj_pos[((size_t)e * N + j) * 2 + 1] == y);
+      if (bad) atomicOr(s.err, ERR_INJECT);
+      L.x0[tid] = L.x[tid] = x;
+      L.y0[tid] = L.y[tid] = y;
+    }
+  } else if (tid < 64) {
+    // x = randint(W), y = randint(L); accept iff grid >= 0 and unoccupied;
+    // candidates are consumed strictly in draw order
+    const int lane = tid;
+    int px = INT32_MIN / 2, py = INT32_MIN / 2, placed = 0;
+    for (int round = 0; round < 256 && placed < N; ++round) {
+      const uint32_t k = (uint32_t)(round * 64 + lane);
+      const uint4 r = philox(s.seed, make_uint4(k, (uint32_t)e, ep, 0x706c6163u));
+      const int cx = (int)bounded(r.x, (uint32_t)s.Wp);
+      const int cy = (int)bounded(r.y, (uint32_t)s.Lp);
+      uint64_t okm = __ballot(!grid_blocked(s, g, cx, cy));
+      while (okm && placed < N) {
+        const int j = __ffsll((unsigned long long)okm) - 1;
+        okm &= okm - 1;
+        const int qx = rdlane(cx, j), qy = rdlane(cy, j);
+        const bool clash = __ballot(lane < placed && px == qx && py == qy) != 0ull;
+        if (!clash) {
+          if (lane == placed) { px = qx; py = qy; }
+          ++placed;
+        }
+      }
+    }
+    if (placed < N && lane == 0) atomicOr(s.err, ERR_PLACEMENT);
+    if (lane < N) {
+      L.x0[lane] = L.x[lane] = px;
+      L.y0[lane] = L.y[lane] = py;
+    }
+  }
+  // the zeroing stores must land before the window stores / atomics below
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  Items I;
+  stage<NT>(s, L, e, /*load_masks=*/false, I);
+  __syncthreads();
+  sense<NT>(s, L);
+  __syncthreads();
+  if (s.sst) { single_tool<NT>(s, L); __syncthreads(); }
+  {
+    const Agents A = load_agents(s, L);
+    merge<NT>(s, L, I, A);
+  }
+  __syncthreads();
+  fold_marks<NT>(s, L);
+  store_words<NT>(s, e, I);
+  __syncthreads();
+  if (tid == 0) {
+    s.free_cnt[e] = L.sc->cnt_free;
+    s.vis_cnt[e] = L.sc->cnt_vis;
+    s.currstep[e] = 0;
+  }
+}
+
+// --------------------------------------------------------------------------
+// obs (dec_grid_rl.py:312-372): layer 0 robot_pad, 1 own free, 2 own obst,
+// E x E around each robot.  Each (agent, layer, row) becomes one E-bit byte
+// in LDS; the uint8 output is then written as dwords.
+// --------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void write_obs(const State& s, const Lds& L, int e, uint8_t* obs_out) {
+  const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc, H = s.H;
+  const uint64_t moved = L.sc->moved;
+  const uint64_t emask = low_mask(E);
+  const Agents A = load_agents(s, L);
+  for (int idx = threadIdx.x; idx < N * Lc * E; idx += NT) {
+    const int a = udiv(idx, s.mg_LcE), rem = idx - a * (Lc * E);
+    const int layer = udiv(rem, s.mg_E), r = rem - layer * E;
+    const int xa = L.x[a], ya = L.y[a];
+    uint64_t bits = 0;
+    if (layer == 0) {
+      const int cx = xa - ego + r, cy0 = ya - ego;
+      for (uint64_t m = moved; m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        const int dc = rdlane(A.y, j) - cy0;
+        if (rdlane(A.x, j) == cx && dc >= 0 && dc < E) bits |= 1ull << dc;
+      }
+    } else if (layer <= 2) {
+      const int er = xa - ego + r - (L.x0[a] - H - 1);
+      const int ec = ya - ego - (L.y0[a] - H - 1);
+      const uint64_t row = (layer == 1 ? L.fold : L.oold)[a * s.We + er];
+      bits = (row >> ec) & emask;
+    }
+    L.obsrow[idx] = (uint8_t)bits;
+  }
+  __syncthreads();
+  const int total = N * Lc * E * E;
+  uint8_t* dst = obs_out + (size_t)e * total;
+  if ((total & 3) == 0) {
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+    for (int i = threadIdx.x; i < total / 4; i += NT) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 4 * i + j;
+        const int row = udiv(q, s.mg_E), col = q - row * E;
+        v |= (uint32_t)((L.obsrow[row] >> col) & 1) << (8 * j);
+      }
+      d32[i] = v;
+    }
+  } else {
+    for (int q = threadIdx.x; q < total; q += NT) {
+      const int row = udiv(q, s.mg_E), col = q - row * E;
+      dst[q] = (uint8_t)((L.obsrow[row] >> col) & 1);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// the env kernel: one workgroup per env
+// --------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_t* __restrict__ actions,
+                                                 const uint8_t* __restrict__ env_mask,
+                                                 const int32_t* __restrict__ inj_pos,
+                                                 double* __restrict__ reward_out,
+                                                 uint8_t* __restrict__ done_out,
+                                                 uint8_t* __restrict__ obs_out,
+                                                 uint8_t* __restrict__ adj_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int N = s.N;
+  const Lds L = carve(smem, s);
+
+  const bool is_step = mode == MODE_STEP;
+  const bool sentinel = is_step && actions[(size_t)e * N] == 255;
+  const bool reset_req = !is_step && (env_mask == nullptr || env_mask[e] != 0);
+  const bool active = is_step && !sentinel;
+
+  STAMP(0);
+  // ---- round trip 1: positions, actions, scalars, beam table ---------------
+  if (tid < N) {
+    const int2 p = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + tid];
+    L.x0[tid] = L.x[tid] = p.x;
+    L.y0[tid] = L.y[tid] = p.y;
+    if (active) L.act[tid] = actions[(size_t)e * N + tid];
+  }
+  if (tid == 0) {
+    const int g = s.env_grid[e];
+    L.sc->grid = g;
+    L.sc->moved = s.moved[e];
+    L.sc->pen = 0.0;
+    L.sc->cnt_free = 0;
+    L.sc->cnt_vis = 0;
+    L.sc->do_reset = 0;
+    if (active) {
+      L.sc->free_old = s.free_cnt[e];
+      L.sc->vis_old = s.vis_cnt[e];
+      L.sc->currstep = s.currstep[e];
+      L.sc->done_thresh = s.done_thresh[e];
+    }
+  }
+  if (s.sensor == 0)
+    for (int b = tid; b < s.nbeams; b += NT) L.beams[b] = s.beams[b];
+  __syncthreads();
+
+  if (active) {
+    STAMP(1);
+    Items I;
+    stage<NT>(s, L, e, true, I);  // ---- round trip 2 ----
+    if (tid == 0) L.sc->numfree = s.numfree[L.sc->grid];
+    __syncthreads();
+    STAMP(2);
+    if (tid < 64) moves(s, L, -s.pen);
+    __syncthreads();
+    STAMP(3);
+    sense<NT>(s, L);
+    __syncthreads();
+    STAMP(4);
+    if (s.sst) { single_tool<NT>(s, L); __syncthreads(); }
+    {
+      const Agents A = load_agents(s, L);
+      merge<NT>(s, L, I, A);
+    }
+    __syncthreads();
+    STAMP(5);
+    if (tid == 0) {
+      Scal* c = L.sc;
+      const uint32_t fc = c->free_old + c->cnt_free;
+      const uint32_t vc = c->vis_old + c->cnt_vis;
+      const int cs = c->currstep + 1;                        // :154
+      double r = c->pen;                                     // :120,132-145
+      r += (double)c->cnt_vis;                               // :151,:256
+      const double pc = (double)fc / (double)c->numfree;     // :552
+      double dt = c->done_thresh;
+      const double thr = (1.0 < dt) ? 1.0 : dt;              // min(done_thresh, 1)
+      const bool covered = thr <= pc;
+      if (covered) r += s.term;                              // :156-157
+      bool done = false;
+      if (covered) { dt += s.dincr; done = true; }           // :540-543
+      else if (cs == s.maxsteps) done = true;                // :544-545
+      reward_out[e] = r;
+      done_out[e] = done ? 1 : 0;
+      s.free_cnt[e] = fc;
+      s.vis_cnt[e] = vc;
+      s.currstep[e] = cs;
+      s.done_thresh[e] = dt;
+      c->do_reset = (done && s.auto_reset) ? 1 : 0;
+    }
+    __syncthreads();
+    STAMP(6);
+    if (!L.sc->do_reset) {
+      fold_marks<NT>(s, L);
+      store_words<NT>(s, e, I);
+      STAMP(7);
+    } else {
+      reset_env<NT>(s, L, e, nullptr);  // the finished episode's words are not stored
+    }
+  } else if (reset_req) {
+    reset_env<NT>(s, L, e, inj_pos);
+  } else {
+    // sentinel step / env left out of a partial reset: obs of the current
+    // state only (dec_grid_rl.py:104-107,160)
+    Items I;
+    stage<NT>(s, L, e, true, I);
+    if (tid == 0 && sentinel) {
+      reward_out[e] = 0.0;
+      done_out[e] = 1;
+    }
+  }
+  __syncthreads();
+
+  if (active || reset_req) {
+    if (tid < N) {
+      reinterpret_cast<int2*>(s.pos)[(size_t)e * N + tid] = make_int2(L.x[tid], L.y[tid]);
+    }
+    if (tid == 0) s.moved[e] = L.sc->moved;
+  }
+  STAMP(8);
+  write_obs<NT>(s, L, e, obs_out);
+  STAMP(9);
+  if (adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
+    uint8_t* ad = adj_out + (size_t)e * N * N;
+    for (int idx = tid; idx < N * N; idx += NT) {
+      const int i = idx / N, j = idx - i * N;
+      const int dx = abs(L.x[i] - L.x[j]), dy = abs(L.y[i] - L.y[j]);
+      ad[idx] = (max(dx, dy) <= s.comm_r) ? 1 : 0;
+    }
+  }
+#ifdef MC_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  STAMP(10);
+}
+
+hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
+                      const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
+                      uint8_t* adj, int nt, hipStream_t stream) {
+  const size_t lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E);
+  dim3 grid(s.B), block(nt);
+#define MC_LAUNCH(T)                                                                          \
+  hipLaunchKernelGGL((env_kernel<T>), grid, block, lds, stream, s, mode, actions, env_mask, \
+                     inj_pos, reward, done, obs, adj)
+  switch (nt) {
+    case 64: MC_LAUNCH(64); break;
+    case 128: MC_LAUNCH(128); break;
+    case 256: MC_LAUNCH(256); break;
+    case 512: MC_LAUNCH(512); break;
+    default: MC_LAUNCH(1024); break;
+  }
+#undef MC_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace mc

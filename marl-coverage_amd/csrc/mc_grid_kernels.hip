@@ -1,0 +1,144 @@
+// mc_grid_kernels.hip — grid-pool upload/generation and map sharing.
+//
+//   pack_grids_kernel: int8 padded grids -> neg/pos bit planes + numfree
+//                      (the np.pad / count_nonzero of dec_grid_rl.py:471,517)
+//   gen_grids_kernel:  Bernoulli obstacle pool (Utils/gridmaker.py:127-128)
+//   share_kernel:      DecGridRL.shareMaps (dec_grid_rl.py:423-447)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mc_device.h"
+
+namespace mc {
+
+// --------------------------------------------------------------------------
+// shareMaps (dec_grid_rl.py:423-447), run before the step kernel when
+// map_sharing is on: agent i's maps <- OR over {j: adj(i,j) or i==j}, with
+// adj from the positions at the start of the step (the last comm graph).
+// grid = (ceil(Wp*nw / 64), B); block = 64 lanes, one word position each.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void share_kernel(State s, const uint8_t* __restrict__ actions) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int e = blockIdx.y;
+  const int N = s.N;
+  if (actions[(size_t)e * N] == 255) return;  // sentinel: no state change
+  const size_t mw = (size_t)s.Wp * s.nw;
+  const int lane = threadIdx.x;
+  const size_t w = (size_t)blockIdx.x * 64 + lane;
+  uint64_t* fo = reinterpret_cast<uint64_t*>(smem);   // [N][64]
+  uint64_t* oo = fo + (size_t)N * 64;                  // [N][64]
+  int32_t* px = reinterpret_cast<int32_t*>(oo + (size_t)N * 64);
+  int32_t* py = px + 64;
+  if (lane < N) {
+    px[lane] = s.pos[((size_t)e * N + lane) * 2];
+    py[lane] = s.pos[((size_t)e * N + lane) * 2 + 1];
+  }
+  uint64_t* f = s.freem + (size_t)e * N * mw + w;
+  uint64_t* o = s.obstm + (size_t)e * N * mw + w;
+  const bool live = w < mw;
+  for (int j = 0; j < N; ++j) {
+    fo[j * 64 + lane] = live ? f[j * mw] : 0ull;
+    oo[j * 64 + lane] = live ? o[j * mw] : 0ull;
+  }
+  __syncthreads();
+  if (!live) return;
+  uint32_t cnt = 0;
+  for (int i = 0; i < N; ++i) {
+    uint64_t fn = 0, on = 0;
+    for (int j = 0; j < N; ++j) {
+      const int d = max(abs(px[i] - px[j]), abs(py[i] - py[j]));
+      if (d <= s.comm_r || i == j) {
+        fn |= fo[j * 64 + lane];
+        on |= oo[j * 64 + lane];
+      }
+    }
+    const uint64_t fi = fo[i * 64 + lane], oi = oo[i * 64 + lane];
+    cnt += __popcll(fn & ~fi);
+    if (fn != fi) f[i * mw] = fn;
+    if (on != oi) o[i * mw] = on;
+  }
+  if (cnt) atomicAdd(&s.free_cnt[e], cnt);
+}
+
+// --------------------------------------------------------------------------
+// grid pool upload / generation
+// --------------------------------------------------------------------------
+// int8 [G][Wp][Lp] -> neg/pos bit planes, numfree[g] = count(grid > 0).
+__global__ void pack_grids_kernel(State s, const int8_t* __restrict__ grids) {
+  const size_t mw = (size_t)s.Wp * s.nw;
+  const size_t total = (size_t)s.G * mw;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i / mw);
+    const size_t rem = i - (size_t)g * mw;
+    const int x = (int)(rem / s.nw), w = (int)(rem - (size_t)x * s.nw);
+    const int8_t* row = grids + ((size_t)g * s.Wp + x) * s.Lp;
+    uint64_t neg = 0, pos = 0;
+    for (int b = 0; b < 64; ++b) {
+      const int y = w * 64 + b;
+      if (y >= s.Lp) { neg |= 1ull << b; continue; }
+      const int8_t v = row[y];
+      if (v < 0) neg |= 1ull << b;
+      if (v > 0) pos |= 1ull << b;
+    }
+    const_cast<uint64_t*>(s.grid_neg)[i] = neg;
+    const_cast<uint64_t*>(s.grid_pos)[i] = pos;
+    if (pos) atomicAdd(const_cast<int32_t*>(&s.numfree[g]), (int32_t)__popcll(pos));
+  }
+}
+
+// Bernoulli(p) obstacles in the interior, -1 border (gridgen semantics,
+// Utils/gridmaker.py:127-128, plus the np.pad of dec_grid_rl.py:471).
+__global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int all_free) {
+  const size_t mw = (size_t)s.Wp * s.nw;
+  const size_t total = (size_t)s.G * mw;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i / mw);
+    const size_t rem = i - (size_t)g * mw;
+    const int x = (int)(rem / s.nw), w = (int)(rem - (size_t)x * s.nw);
+    uint64_t neg = 0;
+    for (int q = 0; q < 16; ++q) {
+      const uint4 r = philox(seed, make_uint4((uint32_t)g, (uint32_t)x, (uint32_t)(w * 16 + q), 0x67656e21u));
+      const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
+      for (int t = 0; t < 4; ++t) {
+        const int b = q * 4 + t;
+        const int y = w * 64 + b;
+        const bool border = x == 0 || x == s.Wp - 1 || y == 0 || y >= s.Lp - 1;
+        if (border || (!all_free && rv[t] < thresh)) neg |= 1ull << b;
+      }
+    }
+    const uint64_t valid = (w == s.nw - 1 && (s.Lp & 63)) ? low_mask(s.Lp & 63) : ~0ull;
+    const uint64_t pos = ~neg & valid;
+    const_cast<uint64_t*>(s.grid_neg)[i] = neg;
+    const_cast<uint64_t*>(s.grid_pos)[i] = pos;
+    if (pos) atomicAdd(const_cast<int32_t*>(&s.numfree[g]), (int32_t)__popcll(pos));
+  }
+}
+
+hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream) {
+  const size_t mw = (size_t)s.Wp * s.nw;
+  dim3 grid((unsigned)((mw + 63) / 64), s.B), block(64);
+  const size_t lds = (size_t)s.N * 64 * 16 + 64 * 8;
+  hipLaunchKernelGGL(share_kernel, grid, block, lds, stream, s, actions);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream) {
+  const size_t total = (size_t)s.G * s.Wp * s.nw;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(pack_grids_kernel, dim3(blocks), dim3(256), 0, stream, s, grids);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream) {
+  const size_t total = (size_t)s.G * s.Wp * s.nw;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  double t = p * 4294967296.0;
+  uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (t <= 0.0 ? 0u : (uint32_t)t);
+  hipLaunchKernelGGL(gen_grids_kernel, dim3(blocks), dim3(256), 0, stream, s, seed, thresh,
+                     p <= 0.0 ? 1 : 0);
+  return hipGetLastError();
+}
+
+}  // namespace mc

@@ -1,0 +1,84 @@
+"""Phase timing of the env kernel from s_memtime stamps (diagnostic build).
+
+    python tools/stamps.py [--envs 4096] [--config c2]
+Builds marl-coverage_amd/libmarlcov_stamps.so with -DMC_STAMPS and prints, per
+phase, the median / p90 / max cycles over all envs of the last step, plus the
+spread of wave start times.  Stamps perturb the schedule: read shares, not
+absolute kernel time.
+"""
+import argparse
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = os.path.join(ROOT, "marl-coverage_amd")
+LIB = os.path.join(PKG, "libmarlcov_stamps.so")
+PHASES = ["rt1 pos/act/scalars", "rt2 stage", "moves", "sense", "merge", "reward",
+          "store", "(reset)", "obs", "adj+drain"]
+
+
+def build(abl=None):
+    import glob
+    srcs = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")))
+    out = LIB if abl is None else LIB.replace(".so", f"_abl{abl}.so")
+    extra = [] if abl is None else [f"-DMC_ABL={abl}"]
+    cmd = ["hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared", "-DMC_STAMPS",
+           *extra, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc"), "-o", out, *srcs]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--abl", type=int, default=None, help="timing ablation build (wrong results)")
+    ap.add_argument("--all-abl", action="store_true", help="also build ablations 1..3")
+    args = ap.parse_args()
+    if args.build_only or not os.path.exists(LIB):
+        build()
+        if args.all_abl:
+            for a in (1, 2, 3):
+                build(a)
+        if args.build_only:
+            return
+    os.environ["MARLCOV_LIB"] = LIB if args.abl is None else LIB.replace(".so", f"_abl{args.abl}.so")
+    print("library:", os.environ["MARLCOV_LIB"])
+    import numpy as np
+    import torch
+    import marlcov
+    from marlcov import _lib
+    import bench
+
+    c = bench.CONFIGS["c2"]
+    cfg = dict(bench.BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"])
+    B = args.envs
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=128, length=128, prob_obst=0.1, seed=1000),
+                                   seed=1, auto_reset=True)
+    st = torch.zeros((B, 16), dtype=torch.int64, device=env.device)
+    _lib.check(env.lib.mc_debug_stamps(env._h, st.data_ptr()), "stamps")
+    env.reset()
+    for t in range(args.steps):
+        a = torch.randint(0, 4, (B, 4), dtype=torch.uint8, device=env.device)
+        env.step(a)
+    torch.cuda.synchronize()
+    s = st.cpu().numpy().astype(np.int64)
+    t0 = s[:, 0].min()
+    print(f"envs={B}  wave start spread (cycles): median {np.median(s[:,0]-t0):.0f}  max {(s[:,0]-t0).max()}")
+    print(f"kernel span (first start -> last end): {s[:,10].max()-t0} cycles")
+    order = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), (7, 8), (8, 9), (9, 10)]
+    for (i, j), name in zip(order, PHASES):
+        ok = (s[:, i] > 0) & (s[:, j] > 0)
+        if not ok.any():
+            print(f"  {name:22s} (no samples)")
+            continue
+        d = s[ok, j] - s[ok, i]
+        print(f"  {name:22s} median {np.median(d):8.0f}  p90 {np.percentile(d,90):8.0f}  max {d.max():8d}  n={ok.sum()}")
+    tot = s[:, 10] - s[:, 0]
+    print(f"  {'whole wave':22s} median {np.median(tot):8.0f}  p90 {np.percentile(tot,90):8.0f}  max {tot.max():8d}")
+
+
+if __name__ == "__main__":
+    main()
