@@ -53,6 +53,15 @@ __device__ __forceinline__ int udiv(int n, uint32_t magic) {
 
 __device__ __forceinline__ int rdlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
+// Window rows are WT = uint32_t when 2H+3 <= 32 (every BASELINE config with
+// range <= 14) and uint64_t otherwise: half the VALU work per bit operation.
+template <typename WT>
+__device__ __forceinline__ WT wmask_of(int w) { return (WT)low_mask(w); }
+__device__ __forceinline__ int popc(uint32_t v) { return __popc(v); }
+__device__ __forceinline__ int popc(uint64_t v) { return __popcll(v); }
+__device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) { atomicOr((unsigned int*)p, v); }
+__device__ __forceinline__ void lds_or(uint64_t* p, uint64_t v) { atomicOr((unsigned long long*)p, v); }
+
 struct Scal {
   double pen;          // move penalties, accumulated in robot order
   double done_thresh;
@@ -67,8 +76,9 @@ struct Scal {
 };
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 
+template <typename WT>
 struct Lds {
-  uint64_t *neg, *pos, *fold, *oold, *fp, *op;
+  WT *neg, *pos, *fold, *oold, *fp, *op;
   Beam* beams;
   int32_t *x0, *y0, *x, *y;
   Scal* sc;
@@ -76,17 +86,18 @@ struct Lds {
   uint8_t* obsrow;  // [N*Lc*E] E-bit crop rows
 };
 
-__device__ __forceinline__ Lds carve(char* smem, const State& s) {
-  Lds L;
+template <typename WT>
+__device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
+  Lds<WT> L;
   const int items = s.N * s.We;
-  uint64_t* p = reinterpret_cast<uint64_t*>(smem);
+  WT* p = reinterpret_cast<WT*>(smem);
   L.neg = p;
   L.pos = p + items;
   L.fold = p + 2 * items;
   L.oold = p + 3 * items;
   L.fp = p + 4 * items;
   L.op = p + 5 * items;
-  char* q = reinterpret_cast<char*>(p + 6 * items);
+  char* q = smem + ((6 * items * sizeof(WT) + 15) & ~(size_t)15);
   L.beams = reinterpret_cast<Beam*>(q);
   q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
   L.x0 = reinterpret_cast<int32_t*>(q);
@@ -109,7 +120,8 @@ struct Agents {
   int x, y;    // post-move
 };
 
-__device__ __forceinline__ Agents load_agents(const State& s, const Lds& L) {
+template <typename WT>
+__device__ __forceinline__ Agents load_agents(const State& s, const Lds<WT>& L) {
   const int j = threadIdx.x & 63;
   Agents A;
   const bool ok = j < s.N;
@@ -122,10 +134,11 @@ __device__ __forceinline__ Agents load_agents(const State& s, const Lds& L) {
 
 // staged (agent, row) items of this lane; raw HBM words stay in registers
 // from stage to store
+template <typename WT>
 struct Items {
   int a[KI], gx[KI], oy[KI];
-  uint64_t f0[KI], f1[KI], o0[KI], o1[KI], u0[KI], u1[KI];
-  uint64_t nf[KI], no[KI], nu[KI];
+  uint64_t f0[KI], f1[KI], o0[KI], o1[KI], u0[KI], u1[KI];  // raw HBM words
+  WT nf[KI], no[KI], nu[KI];                                  // new bits (window)
 };
 
 __device__ __forceinline__ bool row_in(const State& s, int gx) { return gx >= 0 && gx < s.Wp; }
@@ -141,14 +154,14 @@ __device__ __forceinline__ bool word1_in(const State& s, int gx, int oy) {
 // --------------------------------------------------------------------------
 // stage: one round trip for every staged row (masks known zero after reset)
 // --------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void stage(const State& s, const Lds& L, int e, bool load_masks, Items& I) {
+template <int NT, typename WT>
+__device__ __forceinline__ void stage(const State& s, const Lds<WT>& L, int e, bool load_masks, Items<WT>& I) {
   const int items = s.N * s.We;
   const size_t mw = (size_t)s.Wp * s.nw;
   const int g = L.sc->grid;
   const uint64_t* gn = s.grid_neg + (size_t)g * mw;
   const uint64_t* gp = s.grid_pos + (size_t)g * mw;
-  const uint64_t wmask = low_mask(s.We);
+  const uint64_t wmask = low_mask(s.We);  // extraction in u64, stored as WT
   const bool square = s.sensor == 1;
   uint64_t n0[KI], n1[KI], p0[KI], p1[KI];
 #pragma unroll
@@ -198,10 +211,10 @@ __device__ __forceinline__ void stage(const State& s, const Lds& L, int e, bool 
     const int idx = threadIdx.x + k * NT;
     if (idx < items) {
       const int off = I.oy[k] & 63;
-      L.neg[idx] = funnel(n0[k], n1[k], off) & wmask;
-      L.pos[idx] = funnel(p0[k], p1[k], off) & wmask;
-      L.fold[idx] = funnel(I.f0[k], I.f1[k], off) & wmask;
-      L.oold[idx] = funnel(I.o0[k], I.o1[k], off) & wmask;
+      L.neg[idx] = (WT)(funnel(n0[k], n1[k], off) & wmask);
+      L.pos[idx] = (WT)(funnel(p0[k], p1[k], off) & wmask);
+      L.fold[idx] = (WT)(funnel(I.f0[k], I.f1[k], off) & wmask);
+      L.oold[idx] = (WT)(funnel(I.o0[k], I.o1[k], off) & wmask);
       L.fp[idx] = 0;
       L.op[idx] = 0;
     }
@@ -215,7 +228,8 @@ __device__ __forceinline__ void stage(const State& s, const Lds& L, int e, bool 
 // robot that has not moved yet (:186,190-199,310).  The grid test at the
 // target reads the staged extended window (1 outside the grid = isInBounds).
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void moves(const State& s, const Lds& L, double pen_unit) {
+template <typename WT>
+__device__ __forceinline__ void moves(const State& s, const Lds<WT>& L, double pen_unit) {
   const int lane = threadIdx.x;
   const int N = s.N;
   const bool live = lane < N;
@@ -225,8 +239,8 @@ __device__ __forceinline__ void moves(const State& s, const Lds& L, double pen_u
   const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
   int gblk = 1;
   if (live && act < 4) {
-    const uint64_t row = L.neg[lane * s.We + s.H + 1 + dx];
-    gblk = (int)((row >> (s.H + 1 + dy)) & 1ull);
+    const WT row = L.neg[lane * s.We + s.H + 1 + dx];
+    gblk = (int)((row >> (s.H + 1 + dy)) & (WT)1);
   }
   const int tx = x + dx, ty = y + dy;
   double pen = 0.0;
@@ -251,74 +265,64 @@ __device__ __forceinline__ void moves(const State& s, const Lds& L, double pen_u
 // exactly +-1 per step; the minor cell moves by msign at the steps flagged in
 // the host-built beam_bits word for this (beam, start coordinate), which
 // encodes the reference's float64 `+=` chain bit-exactly (mc_internal.h).
-// Two beams per lane advance in lock step; the body is branch-free: both
-// neg-row reads are issued before either mark, and a mark is one ds_or_b64
-// into fp (free) or op (obstacle, ends the beam), with a zero operand once
-// the beam is over.
+// Every cell of a beam lies within Chebyshev K <= H of the post-move robot,
+// which is within 1 of the staged window's centre: no window check is
+// needed (mc_set_beam_table rejects K > H).  Two beams per lane advance in
+// lock step; per step: one LDS read of the neg row and of the free row, and
+// at most one ds_or (free mark, or obstacle mark that ends the beam), skipped
+// when the free bit is already set.
 // --------------------------------------------------------------------------
 struct Ray {
-  uint64_t bits;
-  int r, c, dr, dc, mr, mc, K, base;
+  uint32_t bits;     // minor-move bit per step (K <= 31)
+  int row, col;      // current window cell; LDS row index = base + row
+  int drow, dcol;    // major step
+  int mrow, mcol;    // minor step (when the step's bit is set)
+  int K;
   bool live;
 };
 
-__device__ __forceinline__ Ray ray_init(const State& s, const Lds& L, int idx) {
+template <typename WT>
+__device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int idx) {
   Ray R;
   R.live = idx < s.N * s.nbeams;
   const int a = R.live ? udiv(idx, s.mg_nb) : 0;
   const int b = R.live ? idx - a * s.nbeams : 0;
   const Beam bm = L.beams[b];
   const int xa = L.x[a], ya = L.y[a];
-  R.r = xa - (L.x0[a] - s.H - 1);
-  R.c = ya - (L.y0[a] - s.H - 1);
+  R.row = a * s.We + xa - (L.x0[a] - s.H - 1);
+  R.col = ya - (L.y0[a] - s.H - 1);
   const bool ax = bm.axis == 0;
-  R.dr = ax ? bm.sign : 0;
-  R.dc = ax ? 0 : bm.sign;
-  R.mr = ax ? 0 : bm.msign;
-  R.mc = ax ? bm.msign : 0;
+  R.drow = ax ? bm.sign : 0;
+  R.dcol = ax ? 0 : bm.sign;
+  R.mrow = ax ? 0 : bm.msign;
+  R.mcol = ax ? bm.msign : 0;
   R.K = R.live ? bm.K : -1;
-  R.base = a * s.We;
 #if defined(MC_ABL) && MC_ABL == 2
-  R.bits = 0x5555555555555555ull;  // timing ablation only: no table load
+  R.bits = 0x55555555u;  // timing ablation only: no table load
 #else
-  R.bits = R.live ? s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0ull;
+  R.bits = R.live ? (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0u;
 #endif
   return R;
 }
 
-// cell of step k: window row/col (clamped to 0 when outside the window, with
-// `bad` recording a beam that left it) — independent of earlier hits, so the
-// LDS reads of several steps can be in flight together
-__device__ __forceinline__ void ray_cell(const State& s, const Ray& R, int& r, int& c, bool& inwin) {
-  inwin = (unsigned)R.r < (unsigned)s.We && (unsigned)R.c < (unsigned)s.We;
-  r = inwin ? R.r : 0;
-  c = inwin ? R.c : 0;
-}
-
 __device__ __forceinline__ void ray_advance(Ray& R, int k) {
-  const int mv = (int)((R.bits >> k) & 1ull);
-  R.r += R.dr + mv * R.mr;
-  R.c += R.dc + mv * R.mc;
+  const int mv = (int)((R.bits >> k) & 1u);
+  R.row += R.drow + mv * R.mrow;
+  R.col += R.dcol + mv * R.mcol;
 }
 
-// mark step k (free, or obstacle = end of beam); skip the OR when the free
-// bit is already set (most cells near the robot are hit by many beams)
-__device__ __forceinline__ void ray_mark(const Lds& L, Ray& R, int k, bool inwin, int r, int c,
-                                         uint64_t nrow, uint64_t frow, bool& bad) {
-  const bool run = R.live && k <= R.K;
-  bad |= run && !inwin;
-  const bool on = run && inwin;
-  const uint64_t bit = 1ull << c;
-  const bool hit = (nrow & bit) != 0ull;  // oc[int(cx), int(cy)] < 0
-  if (on && (hit || !(frow & bit))) {
-    uint64_t* dst = (hit ? L.op : L.fp) + R.base + r;
-    atomicOr((unsigned long long*)dst, bit);
-  }
+template <typename WT>
+__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, int row, int col, WT nrow,
+                                         WT frow) {
+  const bool on = R.live && k <= R.K;
+  const WT bit = (WT)1 << col;
+  const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
+  if (on && (hit || !(frow & bit))) lds_or((hit ? L.op : L.fp) + row, bit);
   R.live = on && !hit;
 }
 
-template <int NT>
-__device__ __forceinline__ void sense(const State& s, const Lds& L) {
+template <int NT, typename WT>
+__device__ __forceinline__ void sense(const State& s, const Lds<WT>& L) {
   const int N = s.N, We = s.We, H = s.H;
   if (s.sensor == 0) {
 #if defined(MC_ABL) && MC_ABL == 3
@@ -328,43 +332,35 @@ __device__ __forceinline__ void sense(const State& s, const Lds& L) {
     for (int a = threadIdx.x; a < N; a += NT) {
       const int r0 = L.x[a] - (L.x0[a] - H - 1), c0 = L.y[a] - (L.y0[a] - H - 1);
       if ((unsigned)r0 < (unsigned)We && (unsigned)c0 < (unsigned)We)
-        atomicOr((unsigned long long*)&L.fp[a * We + r0], 1ull << c0);
+        lds_or(&L.fp[a * We + r0], (WT)1 << c0);
     }
     const int total = N * s.nbeams;
-    bool bad = false;
     for (int base = threadIdx.x; base < total; base += 2 * NT) {
-      Ray q0 = ray_init(s, L, base), q1 = ray_init(s, L, base + NT);
+      Ray q0 = ray_init<WT>(s, L, base), q1 = ray_init<WT>(s, L, base + NT);
       ray_advance(q0, 0);
       ray_advance(q1, 0);
       const int kmax = max(q0.K, q1.K);
       for (int k = 1; k <= kmax; k += 2) {
-        // cells of steps k, k+1 for both rays; all eight row reads in flight
-        int ra0, ca0, ra1, ca1, rb0, cb0, rb1, cb1;
-        bool ia0, ia1, ib0, ib1;
-        ray_cell(s, q0, ra0, ca0, ia0);
-        ray_cell(s, q1, ra1, ca1, ia1);
+        // cells of steps k and k+1 of both rays: all eight row reads in flight
         Ray n0 = q0, n1 = q1;
         ray_advance(n0, k);
         ray_advance(n1, k);
-        ray_cell(s, n0, rb0, cb0, ib0);
-        ray_cell(s, n1, rb1, cb1, ib1);
-        const uint64_t na0 = L.neg[q0.base + ra0], fa0 = L.fp[q0.base + ra0];
-        const uint64_t na1 = L.neg[q1.base + ra1], fa1 = L.fp[q1.base + ra1];
-        const uint64_t nb0 = L.neg[q0.base + rb0], fb0 = L.fp[q0.base + rb0];
-        const uint64_t nb1 = L.neg[q1.base + rb1], fb1 = L.fp[q1.base + rb1];
-        ray_mark(L, q0, k, ia0, ra0, ca0, na0, fa0, bad);
-        ray_mark(L, q1, k, ia1, ra1, ca1, na1, fa1, bad);
+        const WT na0 = L.neg[q0.row], fa0 = L.fp[q0.row];
+        const WT na1 = L.neg[q1.row], fa1 = L.fp[q1.row];
+        const WT nb0 = L.neg[n0.row], fb0 = L.fp[n0.row];
+        const WT nb1 = L.neg[n1.row], fb1 = L.fp[n1.row];
+        ray_mark<WT>(L, q0, k, q0.row, q0.col, na0, fa0);
+        ray_mark<WT>(L, q1, k, q1.row, q1.col, na1, fa1);
         n0.live = q0.live;
         n1.live = q1.live;
-        ray_mark(L, n0, k + 1, ib0, rb0, cb0, nb0, fb0, bad);
-        ray_mark(L, n1, k + 1, ib1, rb1, cb1, nb1, fb1, bad);
+        ray_mark<WT>(L, n0, k + 1, n0.row, n0.col, nb0, fb0);
+        ray_mark<WT>(L, n1, k + 1, n1.row, n1.col, nb1, fb1);
         ray_advance(n0, k + 1);
         ray_advance(n1, k + 1);
         q0 = n0;
         q1 = n1;
       }
     }
-    if (bad) atomicOr(s.err, ERR_WINDOW);
   } else {
     // window [x-r, x+r] x [y-r, y+r] clamped to the padded grid; the
     // reference overwrites it with clip(g,0,1) / clip(-g,0,1), which on a
@@ -374,13 +370,13 @@ __device__ __forceinline__ void sense(const State& s, const Lds& L) {
       const int a = udiv(idx, s.mg_We), r = idx - a * We;
       const int ox = L.x0[a] - H - 1, oy = L.y0[a] - H - 1;
       const int gx = ox + r, xa = L.x[a], ya = L.y[a];
-      uint64_t f = 0, o = 0;
+      WT f = 0, o = 0;
       if (gx >= xa - rr && gx <= xa + rr && gx >= 0 && gx < s.Wp) {
         int c0 = ya - rr - oy, c1 = ya + rr - oy;      // extended-window columns
         if (c0 < -oy) c0 = -oy;                          // grid column 0
         if (c1 > s.Lp - 1 - oy) c1 = s.Lp - 1 - oy;      // grid column Lp-1
         if (c1 >= c0) {
-          const uint64_t cm = low_mask(c1 + 1) & ~low_mask(c0);
+          const WT cm = (WT)(low_mask(c1 + 1) & ~low_mask(c0));
           f = L.pos[idx] & cm;
           o = L.neg[idx] & cm;
         }
@@ -392,12 +388,12 @@ __device__ __forceinline__ void sense(const State& s, const Lds& L) {
 }
 
 // single_square_tool: only the robot's own cell becomes free (:233-234)
-template <int NT>
-__device__ __forceinline__ void single_tool(const State& s, const Lds& L) {
+template <int NT, typename WT>
+__device__ __forceinline__ void single_tool(const State& s, const Lds<WT>& L) {
   for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
     const int a = udiv(idx, s.mg_We), r = idx - a * s.We;
     const int ox = L.x0[a] - s.H - 1, oy = L.y0[a] - s.H - 1;
-    L.fp[idx] = (ox + r == L.x[a]) ? (1ull << (L.y[a] - oy)) : 0ull;
+    L.fp[idx] = (ox + r == L.x[a]) ? ((WT)1 << (L.y[a] - oy)) : (WT)0;
   }
 }
 
@@ -406,8 +402,8 @@ __device__ __forceinline__ void single_tool(const State& s, const Lds& L) {
 // union delta = cells some agent marked this step that were not yet visited,
 // each counted at the lowest-index agent that marked it.
 // --------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void merge(const State& s, const Lds& L, Items& I, const Agents& A) {
+template <int NT, typename WT>
+__device__ __forceinline__ void merge(const State& s, const Lds<WT>& L, Items<WT>& I, const Agents& A) {
   const int items = s.N * s.We;
   const uint64_t wmask = low_mask(s.We);
   uint32_t cf = 0, cv = 0;
@@ -416,25 +412,25 @@ __device__ __forceinline__ void merge(const State& s, const Lds& L, Items& I, co
     const int idx = threadIdx.x + k * NT;
     I.nf[k] = I.no[k] = I.nu[k] = 0;
     if (idx < items) {
-      const uint64_t fp = L.fp[idx], op = L.op[idx];
+      const WT fp = L.fp[idx], op = L.op[idx];
       I.nf[k] = fp & ~L.fold[idx];
       I.no[k] = op & ~L.oold[idx];
-      cf += __popcll(I.nf[k]);
+      cf += popc(I.nf[k]);
       const int a = I.a[k], gx = I.gx[k], oy = I.oy[k];
-      uint64_t cand = fp & ~(funnel(I.u0[k], I.u1[k], oy & 63) & wmask);
+      WT cand = fp & ~(WT)(funnel(I.u0[k], I.u1[k], oy & 63) & wmask);
       if (cand) {
         for (int b = 0; b < s.N; ++b) {  // marks of lower-index agents at these cells
           const int xb = rdlane(A.x0, b), yb = rdlane(A.y0, b);
           const int rb = gx - (xb - s.H - 1);
           const int d = (yb - s.H - 1) - oy;  // column shift b -> a (|d| < We to overlap)
           if (b < a && (unsigned)rb < (unsigned)s.We && d > -s.We && d < s.We) {
-            const uint64_t pb = L.fp[b * s.We + rb];
+            const WT pb = L.fp[b * s.We + rb];
             cand &= ~(d >= 0 ? (pb << d) : (pb >> -d));
           }
         }
       }
       I.nu[k] = cand;
-      cv += __popcll(cand);
+      cv += popc(cand);
     }
   }
   if (cf) atomicAdd(&L.sc->cnt_free, cf);
@@ -442,16 +438,16 @@ __device__ __forceinline__ void merge(const State& s, const Lds& L, Items& I, co
 }
 
 // after merge: fold |= fp (obs crops read the post-step maps)
-template <int NT>
-__device__ __forceinline__ void fold_marks(const State& s, const Lds& L) {
+template <int NT, typename WT>
+__device__ __forceinline__ void fold_marks(const State& s, const Lds<WT>& L) {
   for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
     L.fold[idx] |= L.fp[idx];
     L.oold[idx] |= L.op[idx];
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void store_words(const State& s, int e, const Items& I) {
+template <int NT, typename WT>
+__device__ __forceinline__ void store_words(const State& s, int e, const Items<WT>& I) {
   const int items = s.N * s.We;
   const size_t mw = (size_t)s.Wp * s.nw;
 #pragma unroll
@@ -464,7 +460,7 @@ __device__ __forceinline__ void store_words(const State& s, int e, const Items& 
     const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
     const size_t rb = (size_t)gx * s.nw;
     const size_t fb = ((size_t)e * s.N + I.a[k]) * mw + rb;
-    const uint64_t nf = I.nf[k], no = I.no[k], nu = I.nu[k];
+    const uint64_t nf = I.nf[k], no = I.no[k], nu = I.nu[k];  // widened to the HBM word
     if (nf) {
       if (in0) s.freem[fb + w0] = I.f0[k] | (nf << off);
       if (in1) s.freem[fb + w0 + 1] = I.f1[k] | (nf >> (64 - off));
@@ -486,8 +482,8 @@ __device__ __forceinline__ void store_words(const State& s, int e, const Items& 
 // cells (injected, or Philox rejection draw with the reference's acceptance
 // rule, :491-502), zeroed maps, initial observe() (reward discarded, :524).
 // --------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void reset_env(const State& s, const Lds& L, int e, const int32_t* inj_pos) {
+template <int NT, typename WT>
+__device__ __forceinline__ void reset_env(const State& s, const Lds<WT>& L, int e, const int32_t* inj_pos) {
   const int N = s.N;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -557,19 +553,19 @@ __device__ __forceinline__ void reset_env(const State& s, const Lds& L, int e, c
   // the zeroing stores must land before the window stores / atomics below
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  Items I;
-  stage<NT>(s, L, e, /*load_masks=*/false, I);
+  Items<WT> I;
+  stage<NT, WT>(s, L, e, /*load_masks=*/false, I);
   __syncthreads();
-  sense<NT>(s, L);
+  sense<NT, WT>(s, L);
   __syncthreads();
-  if (s.sst) { single_tool<NT>(s, L); __syncthreads(); }
+  if (s.sst) { single_tool<NT, WT>(s, L); __syncthreads(); }
   {
-    const Agents A = load_agents(s, L);
-    merge<NT>(s, L, I, A);
+    const Agents A = load_agents<WT>(s, L);
+    merge<NT, WT>(s, L, I, A);
   }
   __syncthreads();
-  fold_marks<NT>(s, L);
-  store_words<NT>(s, e, I);
+  fold_marks<NT, WT>(s, L);
+  store_words<NT, WT>(s, e, I);
   __syncthreads();
   if (tid == 0) {
     s.free_cnt[e] = L.sc->cnt_free;
@@ -583,28 +579,28 @@ __device__ __forceinline__ void reset_env(const State& s, const Lds& L, int e, c
 // E x E around each robot.  Each (agent, layer, row) becomes one E-bit byte
 // in LDS; the uint8 output is then written as dwords.
 // --------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void write_obs(const State& s, const Lds& L, int e, uint8_t* obs_out) {
+template <int NT, typename WT>
+__device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int e, uint8_t* obs_out) {
   const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc, H = s.H;
   const uint64_t moved = L.sc->moved;
-  const uint64_t emask = low_mask(E);
-  const Agents A = load_agents(s, L);
+  const WT emask = wmask_of<WT>(E);
+  const Agents A = load_agents<WT>(s, L);
   for (int idx = threadIdx.x; idx < N * Lc * E; idx += NT) {
     const int a = udiv(idx, s.mg_LcE), rem = idx - a * (Lc * E);
     const int layer = udiv(rem, s.mg_E), r = rem - layer * E;
     const int xa = L.x[a], ya = L.y[a];
-    uint64_t bits = 0;
+    WT bits = 0;
     if (layer == 0) {
       const int cx = xa - ego + r, cy0 = ya - ego;
       for (uint64_t m = moved; m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
         const int dc = rdlane(A.y, j) - cy0;
-        if (rdlane(A.x, j) == cx && dc >= 0 && dc < E) bits |= 1ull << dc;
+        if (rdlane(A.x, j) == cx && dc >= 0 && dc < E) bits |= (WT)1 << dc;
       }
     } else if (layer <= 2) {
       const int er = xa - ego + r - (L.x0[a] - H - 1);
       const int ec = ya - ego - (L.y0[a] - H - 1);
-      const uint64_t row = (layer == 1 ? L.fold : L.oold)[a * s.We + er];
+      const WT row = (layer == 1 ? L.fold : L.oold)[a * s.We + er];
       bits = (row >> ec) & emask;
     }
     L.obsrow[idx] = (uint8_t)bits;
@@ -635,7 +631,7 @@ __device__ __forceinline__ void write_obs(const State& s, const Lds& L, int e, u
 // --------------------------------------------------------------------------
 // the env kernel: one workgroup per env
 // --------------------------------------------------------------------------
-template <int NT>
+template <int NT, typename WT>
 __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ env_mask,
                                                  const int32_t* __restrict__ inj_pos,
@@ -647,7 +643,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
   const int e = blockIdx.x;
   const int tid = threadIdx.x;
   const int N = s.N;
-  const Lds L = carve(smem, s);
+  const Lds<WT> L = carve<WT>(smem, s);
 
   const bool is_step = mode == MODE_STEP;
   const bool sentinel = is_step && actions[(size_t)e * N] == 255;
@@ -683,21 +679,21 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
 
   if (active) {
     STAMP(1);
-    Items I;
-    stage<NT>(s, L, e, true, I);  // ---- round trip 2 ----
+    Items<WT> I;
+    stage<NT, WT>(s, L, e, true, I);  // ---- round trip 2 ----
     if (tid == 0) L.sc->numfree = s.numfree[L.sc->grid];
     __syncthreads();
     STAMP(2);
-    if (tid < 64) moves(s, L, -s.pen);
+    if (tid < 64) moves<WT>(s, L, -s.pen);
     __syncthreads();
     STAMP(3);
-    sense<NT>(s, L);
+    sense<NT, WT>(s, L);
     __syncthreads();
     STAMP(4);
-    if (s.sst) { single_tool<NT>(s, L); __syncthreads(); }
+    if (s.sst) { single_tool<NT, WT>(s, L); __syncthreads(); }
     {
-      const Agents A = load_agents(s, L);
-      merge<NT>(s, L, I, A);
+      const Agents A = load_agents<WT>(s, L);
+      merge<NT, WT>(s, L, I, A);
     }
     __syncthreads();
     STAMP(5);
@@ -727,19 +723,19 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     __syncthreads();
     STAMP(6);
     if (!L.sc->do_reset) {
-      fold_marks<NT>(s, L);
-      store_words<NT>(s, e, I);
+      fold_marks<NT, WT>(s, L);
+      store_words<NT, WT>(s, e, I);
       STAMP(7);
     } else {
-      reset_env<NT>(s, L, e, nullptr);  // the finished episode's words are not stored
+      reset_env<NT, WT>(s, L, e, nullptr);  // the finished episode's words are not stored
     }
   } else if (reset_req) {
-    reset_env<NT>(s, L, e, inj_pos);
+    reset_env<NT, WT>(s, L, e, inj_pos);
   } else {
     // sentinel step / env left out of a partial reset: obs of the current
     // state only (dec_grid_rl.py:104-107,160)
-    Items I;
-    stage<NT>(s, L, e, true, I);
+    Items<WT> I;
+    stage<NT, WT>(s, L, e, true, I);
     if (tid == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
@@ -754,7 +750,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     if (tid == 0) s.moved[e] = L.sc->moved;
   }
   STAMP(8);
-  write_obs<NT>(s, L, e, obs_out);
+  write_obs<NT, WT>(s, L, e, obs_out);
   STAMP(9);
   if (adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
     uint8_t* ad = adj_out + (size_t)e * N * N;
@@ -773,17 +769,29 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
 hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
                       uint8_t* adj, int nt, hipStream_t stream) {
-  const size_t lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E);
+  const bool narrow = s.We <= 32;
+  const size_t lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
+                                   narrow ? 4 : 8);
   dim3 grid(s.B), block(nt);
-#define MC_LAUNCH(T)                                                                          \
-  hipLaunchKernelGGL((env_kernel<T>), grid, block, lds, stream, s, mode, actions, env_mask, \
+#define MC_LAUNCH(T, W)                                                                          \
+  hipLaunchKernelGGL((env_kernel<T, W>), grid, block, lds, stream, s, mode, actions, env_mask, \
                      inj_pos, reward, done, obs, adj)
-  switch (nt) {
-    case 64: MC_LAUNCH(64); break;
-    case 128: MC_LAUNCH(128); break;
-    case 256: MC_LAUNCH(256); break;
-    case 512: MC_LAUNCH(512); break;
-    default: MC_LAUNCH(1024); break;
+  if (narrow) {
+    switch (nt) {
+      case 64: MC_LAUNCH(64, uint32_t); break;
+      case 128: MC_LAUNCH(128, uint32_t); break;
+      case 256: MC_LAUNCH(256, uint32_t); break;
+      case 512: MC_LAUNCH(512, uint32_t); break;
+      default: MC_LAUNCH(1024, uint32_t); break;
+    }
+  } else {
+    switch (nt) {
+      case 64: MC_LAUNCH(64, uint64_t); break;
+      case 128: MC_LAUNCH(128, uint64_t); break;
+      case 256: MC_LAUNCH(256, uint64_t); break;
+      case 512: MC_LAUNCH(512, uint64_t); break;
+      default: MC_LAUNCH(1024, uint64_t); break;
+    }
   }
 #undef MC_LAUNCH
   return hipGetLastError();

@@ -81,9 +81,10 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, row) items per lane
 inline uint32_t magic_div(uint32_t d) { return d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d); }
 
 // LDS bytes of the env kernel (host + device use the same carve).
-__host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int Lc, int E) {
+__host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int Lc, int E,
+                                                size_t wbytes) {
   const size_t items = (size_t)N * We;
-  size_t b = 6 * items * 8;                  // neg, pos, fold, oold, fp, op
+  size_t b = (6 * items * wbytes + 15) & ~(size_t)15;  // neg, pos, fold, oold, fp, op
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;  // beams
   b += (size_t)N * 16;                       // x0, y0, x, y
   b += 64;                                   // scalars
