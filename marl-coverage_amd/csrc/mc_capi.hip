@@ -18,7 +18,8 @@
 namespace mc {
 hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
-                      uint8_t* adj, int nt, hipStream_t stream);
+                      uint8_t* adj, int nt, int epw, hipStream_t stream);
+int env_pack(const State& s);
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream);
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
@@ -52,6 +53,7 @@ struct Env {
   mc::State s;
   int device = 0;
   int nt = 128;
+  int epw = 1;  // envs per workgroup (2: two envs share one wave)
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
   void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
@@ -109,6 +111,16 @@ int env_threads(const mc::State& s) {
 }
 
 Env* as_env(void* p) { return static_cast<Env*>(p); }
+
+// envs per workgroup for this launch; MARLCOV_EPW=1 forces one env per
+// workgroup (A/B tuning)
+int launch_epw(const Env* E) {
+  static const int force1 = [] {
+    const char* v = getenv("MARLCOV_EPW");
+    return v && atoi(v) == 1;
+  }();
+  return force1 ? 1 : E->epw;
+}
 
 }  // namespace
 
@@ -255,6 +267,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     const int v = atoi(ov);
     if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) E->nt = v > E->nt ? v : E->nt;
   }
+  E->epw = mc::env_pack(s);
   mc_layout& L = E->lay;
   L.words_per_row = s.nw;
   L.window_half = s.H;
@@ -353,6 +366,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     E->s.mg_nb = mc::magic_div((uint32_t)num_beams);
     E->cfg.num_beams = num_beams;
     E->nt = env_threads(E->s);
+    E->epw = mc::env_pack(E->s);
   }
   HIP_TRY(hipMemcpy((void*)E->s.beams, bt.data(), (size_t)num_beams * sizeof(mc::Beam),
                     hipMemcpyHostToDevice));
@@ -422,7 +436,7 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, voi
   if (rc) return rc;
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(mc::launch_env(E->s, mc::MODE_RESET, nullptr, dev_env_mask, dev_pos, nullptr, nullptr,
-                         (uint8_t*)dev_obs, dev_adj, E->nt, (hipStream_t)stream));
+                         (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), (hipStream_t)stream));
   return MC_OK;
 }
 
@@ -437,7 +451,7 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* 
   HIP_TRY(hipSetDevice(E->device));
   if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
   HIP_TRY(mc::launch_env(E->s, mc::MODE_STEP, dev_actions, nullptr, nullptr, dev_reward, dev_done,
-                         (uint8_t*)dev_obs, dev_adj, E->nt, st));
+                         (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), st));
   return MC_OK;
 }
 

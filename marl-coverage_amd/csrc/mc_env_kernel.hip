@@ -5,23 +5,24 @@
 //   Environments/Sensors/lidar.py LidarSensor.getMeasurement :16-65
 //   Environments/Sensors/squaresensor.py SquareSensor.getMeasurement :15-37
 //
-// One workgroup = one env (one wave for the BASELINE configs).  Per step:
+// A workgroup runs EPW envs ("slots"), LPE = NT / EPW lanes each.  Small envs
+// (the BASELINE configs) pack two envs into one wave: every wave-wide
+// instruction then serves two envs, which matters because the step is VALU
+// issue bound.  Per env and step:
 //   round trip 1  positions, actions, per-env scalars
 //   round trip 2  for every agent the (2H+3)-row "extended window" around its
 //                 pre-move cell: grid neg/pos bits, its free/obst mask words,
 //                 the union (visited) words — 2 u64 per row and plane.  The
 //                 +1 margin covers every post-move window, so the sequential
 //                 moves, the beam march and the merge need no further loads.
-//   LDS compute   moves (wave-serial in robot order, readlane/ballot), lidar or
-//                 square sensing as LDS bit tests + ds_or_b64 marks (two beams
-//                 interleaved per lane), merge with popcounts
+//   LDS compute   moves (slot-serial in robot order), lidar or square sensing
+//                 as LDS bit tests + ds_or marks, merge with popcounts
 //   stores        changed mask words (plain stores: one writer per word),
 //                 newly covered union bits (global_atomic_or: agents' windows
 //                 overlap), positions, counters, reward, done, obs
-// All float64 arithmetic is the reference's: the minor beam coordinate is a
-// sequential `+=` from the robot cell (adds only: nothing to contract into an
-// FMA); the major coordinate moves by exactly +-1 (|inc| == 1 after the
-// normalisation of lidar.py:43-45); rewards are assembled in reference order.
+// All float64 arithmetic is the reference's: rewards are assembled in
+// reference order; the beam's float64 `+=` chain is encoded bit-exactly in
+// the host-built step bits (mc_internal.h, struct Beam).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,21 +31,19 @@
 namespace mc {
 
 #ifdef MC_STAMPS
-#define STAMP(k)                                                                       \
-  do {                                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
-    uint64_t _t;                                                                       \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
-    if (threadIdx.x == 0 && s.stamps) s.stamps[(size_t)blockIdx.x * 16 + (k)] = _t;    \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    uint64_t _t;                                                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
+    if (threadIdx.x == 0 && s.stamps) s.stamps[(size_t)blockIdx.x * EPW * 16 + (k)] = _t; \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
   } while (0)
 #else
 #define STAMP(k) \
   do {           \
   } while (0)
 #endif
-
-constexpr int KI = kMaxItemsPerLane;
 
 // n / d via the magic reciprocal of mc_internal.h (magic == 0 encodes d == 1)
 __device__ __forceinline__ int udiv(int n, uint32_t magic) {
@@ -54,7 +53,7 @@ __device__ __forceinline__ int udiv(int n, uint32_t magic) {
 __device__ __forceinline__ int rdlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
 // Window rows are WT = uint32_t when 2H+3 <= 32 (every BASELINE config with
-// range <= 14) and uint64_t otherwise: half the VALU work per bit operation.
+// range <= 14) and uint64_t otherwise.
 template <typename WT>
 __device__ __forceinline__ WT wmask_of(int w) { return (WT)low_mask(w); }
 __device__ __forceinline__ int popc(uint32_t v) { return __popc(v); }
@@ -113,28 +112,36 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   return L;
 }
 
-// Per lane: agent (lane % 64)'s cells in registers, so loops over agents use
-// v_readlane (SGPR) instead of LDS round trips.  N <= 64.
-struct Agents {
-  int x0, y0;  // pre-move (extended-window origin basis)
-  int x, y;    // post-move
+// one env slot of the workgroup
+template <int NT, int EPW, typename WT>
+struct Ctx {
+  static constexpr int LPE = NT / EPW;            // lanes per env
+  static constexpr int KI = EPW == 1 ? 2 : 3;     // staged items per lane
+  static constexpr int RPL = EPW == 1 ? 2 : 3;    // beams per lane per pass
+  int sub;    // lane within the env
+  int lane0;  // first lane of this env's slot within the wave
+  int e;      // env index
+  Lds<WT> L;
 };
 
-template <typename WT>
-__device__ __forceinline__ Agents load_agents(const State& s, const Lds<WT>& L) {
-  const int j = threadIdx.x & 63;
-  Agents A;
-  const bool ok = j < s.N;
-  A.x0 = ok ? L.x0[j] : 0;
-  A.y0 = ok ? L.y0[j] : 0;
-  A.x = ok ? L.x[j] : 0;
-  A.y = ok ? L.y[j] : 0;
-  return A;
+// broadcast lane (lane0 + i)'s value of v to the slot
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ int bcast(const Ctx<NT, EPW, WT>& C, int v, int i) {
+  if constexpr (EPW == 1) return rdlane(v, i);
+  else return __shfl(v, C.lane0 + i);
+}
+
+// ballot restricted to this env's slot (bit j = lane lane0 + j)
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ uint64_t slot_ballot(const Ctx<NT, EPW, WT>& C, bool p) {
+  const uint64_t m = __ballot(p);
+  if constexpr (EPW == 1) return m;
+  else return (m >> C.lane0) & low_mask(Ctx<NT, EPW, WT>::LPE);
 }
 
 // staged (agent, row) items of this lane; raw HBM words stay in registers
 // from stage to store
-template <typename WT>
+template <int KI, typename WT>
 struct Items {
   int a[KI], gx[KI], oy[KI];
   uint64_t f0[KI], f1[KI], o0[KI], o1[KI], u0[KI], u1[KI];  // raw HBM words
@@ -154,19 +161,22 @@ __device__ __forceinline__ bool word1_in(const State& s, int gx, int oy) {
 // --------------------------------------------------------------------------
 // stage: one round trip for every staged row (masks known zero after reset)
 // --------------------------------------------------------------------------
-template <int NT, typename WT>
-__device__ __forceinline__ void stage(const State& s, const Lds<WT>& L, int e, bool load_masks, Items<WT>& I) {
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, bool load_masks,
+                                      Items<KI, WT>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int items = s.N * s.We;
   const size_t mw = (size_t)s.Wp * s.nw;
   const int g = L.sc->grid;
   const uint64_t* gn = s.grid_neg + (size_t)g * mw;
   const uint64_t* gp = s.grid_pos + (size_t)g * mw;
-  const uint64_t wmask = low_mask(s.We);  // extraction in u64, stored as WT
+  const uint64_t wmask = low_mask(s.We);
   const bool square = s.sensor == 1;
   uint64_t n0[KI], n1[KI], p0[KI], p1[KI];
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
-    const int idx = threadIdx.x + k * NT;
+    const int idx = C.sub + k * LPE;
     n0[k] = n1[k] = ~0ull;
     p0[k] = p1[k] = 0;
     I.f0[k] = I.f1[k] = I.o0[k] = I.o1[k] = I.u0[k] = I.u1[k] = 0;
@@ -184,8 +194,8 @@ __device__ __forceinline__ void stage(const State& s, const Lds<WT>& L, int e, b
       const int w0 = oy >> 6;
       const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
       const size_t rb = (size_t)(row_in(s, gx) ? gx : 0) * s.nw;
-      const size_t fb = ((size_t)e * s.N + a) * mw + rb;
-      const size_t vb = (size_t)e * mw + rb;
+      const size_t fb = ((size_t)C.e * s.N + a) * mw + rb;
+      const size_t vb = (size_t)C.e * mw + rb;
       if (in0) {
         n0[k] = gn[rb + w0];
         if (square) p0[k] = gp[rb + w0];
@@ -208,7 +218,7 @@ __device__ __forceinline__ void stage(const State& s, const Lds<WT>& L, int e, b
   }
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
-    const int idx = threadIdx.x + k * NT;
+    const int idx = C.sub + k * LPE;
     if (idx < items) {
       const int off = I.oy[k] & 63;
       L.neg[idx] = (WT)(funnel(n0[k], n1[k], off) & wmask);
@@ -223,41 +233,39 @@ __device__ __forceinline__ void stage(const State& s, const Lds<WT>& L, int e, b
 
 // --------------------------------------------------------------------------
 // moves: updateRobotPos in robot order (dec_grid_rl.py:128-145, :171-204).
-// Wave 0, lane i = robot i.  Occupancy is the live position set: a robot may
-// enter a cell vacated earlier in this step and is blocked by a higher-index
-// robot that has not moved yet (:186,190-199,310).  The grid test at the
-// target reads the staged extended window (1 outside the grid = isInBounds).
+// Lane lane0+i = robot i of the slot.  Occupancy is the live position set: a
+// robot may enter a cell vacated earlier in this step and is blocked by a
+// higher-index robot that has not moved yet (:186,190-199,310).  The grid
+// test reads the staged extended window (1 outside the grid = isInBounds).
 // --------------------------------------------------------------------------
-template <typename WT>
-__device__ __forceinline__ void moves(const State& s, const Lds<WT>& L, double pen_unit) {
-  const int lane = threadIdx.x;
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C, double pen_unit) {
+  const Lds<WT>& L = C.L;
   const int N = s.N;
-  const bool live = lane < N;
-  int x = live ? L.x0[lane] : INT32_MIN / 2;
-  int y = live ? L.y0[lane] : INT32_MIN / 2;
-  const int act = live ? (int)L.act[lane] : 255;
+  const bool live = C.sub < N;
+  int x = live ? L.x0[C.sub] : INT32_MIN / 2;
+  int y = live ? L.y0[C.sub] : INT32_MIN / 2;
+  const int act = live ? (int)L.act[C.sub] : 255;
   const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
   int gblk = 1;
   if (live && act < 4) {
-    const WT row = L.neg[lane * s.We + s.H + 1 + dx];
+    const WT row = L.neg[C.sub * s.We + s.H + 1 + dx];
     gblk = (int)((row >> (s.H + 1 + dy)) & (WT)1);
   }
   const int tx = x + dx, ty = y + dy;
   double pen = 0.0;
   uint64_t moved = L.sc->moved;
   for (int i = 0; i < N; ++i) {
-    if (rdlane(act, i) > 3) continue;  // not 0..3: no updateRobotPos call, no penalty
-    const int txi = rdlane(tx, i), tyi = rdlane(ty, i);
-    const bool occ = __ballot(live && x == txi && y == tyi) != 0ull;
-    if (!rdlane(gblk, i) && !occ) {
-      if (lane == i) { x = txi; y = tyi; }
-      moved |= 1ull << i;
-    } else {
-      pen += pen_unit;  // reward += -collision_penalty (:203)
-    }
+    const bool acts = bcast(C, act, i) <= 3;  // not 0..3: no updateRobotPos call, no penalty
+    const int txi = bcast(C, tx, i), tyi = bcast(C, ty, i);
+    const bool occ = slot_ballot(C, live && x == txi && y == tyi) != 0ull;
+    const bool ok = acts && !bcast(C, gblk, i) && !occ;
+    if (ok && C.sub == i) { x = txi; y = tyi; }
+    if (ok) moved |= 1ull << i;
+    if (acts && !ok) pen += pen_unit;  // reward += -collision_penalty (:203)
   }
-  if (live) { L.x[lane] = x; L.y[lane] = y; }
-  if (lane == 0) { L.sc->pen = pen; L.sc->moved = moved; }
+  if (live) { L.x[C.sub] = x; L.y[C.sub] = y; }
+  if (C.sub == 0) { L.sc->pen = pen; L.sc->moved = moved; }
 }
 
 // --------------------------------------------------------------------------
@@ -267,14 +275,14 @@ __device__ __forceinline__ void moves(const State& s, const Lds<WT>& L, double p
 // encodes the reference's float64 `+=` chain bit-exactly (mc_internal.h).
 // Every cell of a beam lies within Chebyshev K <= H of the post-move robot,
 // which is within 1 of the staged window's centre: no window check is
-// needed (mc_set_beam_table rejects K > H).  Two beams per lane advance in
+// needed (mc_set_beam_table rejects K > H).  RPL beams per lane advance in
 // lock step; per step: one LDS read of the neg row and of the free row, and
 // at most one ds_or (free mark, or obstacle mark that ends the beam), skipped
 // when the free bit is already set.
 // --------------------------------------------------------------------------
 struct Ray {
   uint32_t bits;     // minor-move bit per step (K <= 31)
-  int row, col;      // current window cell; LDS row index = base + row
+  int row, col;      // current window cell; LDS row index = agent base + row
   int drow, dcol;    // major step
   int mrow, mcol;    // minor step (when the step's bit is set)
   int K;
@@ -297,11 +305,7 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   R.mrow = ax ? 0 : bm.msign;
   R.mcol = ax ? bm.msign : 0;
   R.K = R.live ? bm.K : -1;
-#if defined(MC_ABL) && MC_ABL == 2
-  R.bits = 0x55555555u;  // timing ablation only: no table load
-#else
   R.bits = R.live ? (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0u;
-#endif
   return R;
 }
 
@@ -312,53 +316,48 @@ __device__ __forceinline__ void ray_advance(Ray& R, int k) {
 }
 
 template <typename WT>
-__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, int row, int col, WT nrow,
-                                         WT frow) {
+__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow) {
   const bool on = R.live && k <= R.K;
-  const WT bit = (WT)1 << col;
+  const WT bit = (WT)1 << R.col;
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
-  if (on && (hit || !(frow & bit))) lds_or((hit ? L.op : L.fp) + row, bit);
+  if (on && (hit || !(frow & bit))) lds_or((hit ? L.op : L.fp) + R.row, bit);
   R.live = on && !hit;
 }
 
-template <int NT, typename WT>
-__device__ __forceinline__ void sense(const State& s, const Lds<WT>& L) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int RPL = Ctx<NT, EPW, WT>::RPL;
+  const Lds<WT>& L = C.L;
   const int N = s.N, We = s.We, H = s.H;
   if (s.sensor == 0) {
-#if defined(MC_ABL) && MC_ABL == 3
-    return;  // timing ablation only: no march
-#endif
     // step 0 of every beam is the robot's own (free) cell: mark it once
-    for (int a = threadIdx.x; a < N; a += NT) {
+    for (int a = C.sub; a < N; a += LPE) {
       const int r0 = L.x[a] - (L.x0[a] - H - 1), c0 = L.y[a] - (L.y0[a] - H - 1);
-      if ((unsigned)r0 < (unsigned)We && (unsigned)c0 < (unsigned)We)
-        lds_or(&L.fp[a * We + r0], (WT)1 << c0);
+      lds_or(&L.fp[a * We + r0], (WT)1 << c0);
     }
     const int total = N * s.nbeams;
-    for (int base = threadIdx.x; base < total; base += 2 * NT) {
-      Ray q0 = ray_init<WT>(s, L, base), q1 = ray_init<WT>(s, L, base + NT);
-      ray_advance(q0, 0);
-      ray_advance(q1, 0);
-      const int kmax = max(q0.K, q1.K);
-      for (int k = 1; k <= kmax; k += 2) {
-        // cells of steps k and k+1 of both rays: all eight row reads in flight
-        Ray n0 = q0, n1 = q1;
-        ray_advance(n0, k);
-        ray_advance(n1, k);
-        const WT na0 = L.neg[q0.row], fa0 = L.fp[q0.row];
-        const WT na1 = L.neg[q1.row], fa1 = L.fp[q1.row];
-        const WT nb0 = L.neg[n0.row], fb0 = L.fp[n0.row];
-        const WT nb1 = L.neg[n1.row], fb1 = L.fp[n1.row];
-        ray_mark<WT>(L, q0, k, q0.row, q0.col, na0, fa0);
-        ray_mark<WT>(L, q1, k, q1.row, q1.col, na1, fa1);
-        n0.live = q0.live;
-        n1.live = q1.live;
-        ray_mark<WT>(L, n0, k + 1, n0.row, n0.col, nb0, fb0);
-        ray_mark<WT>(L, n1, k + 1, n1.row, n1.col, nb1, fb1);
-        ray_advance(n0, k + 1);
-        ray_advance(n1, k + 1);
-        q0 = n0;
-        q1 = n1;
+    for (int base = C.sub; base < total; base += RPL * LPE) {
+      Ray q[RPL];
+      int kmax = 0;
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        q[j] = ray_init<WT>(s, L, base + j * LPE);
+        ray_advance(q[j], 0);
+        kmax = max(kmax, q[j].K);
+      }
+      for (int k = 1; k <= kmax; ++k) {
+        WT nr[RPL], fr[RPL];
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {  // all row reads of this step in flight
+          nr[j] = L.neg[q[j].row];
+          fr[j] = L.fp[q[j].row];
+        }
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+          ray_mark<WT>(L, q[j], k, nr[j], fr[j]);
+          ray_advance(q[j], k);
+        }
       }
     }
   } else {
@@ -366,7 +365,7 @@ __device__ __forceinline__ void sense(const State& s, const Lds<WT>& L) {
     // reference overwrites it with clip(g,0,1) / clip(-g,0,1), which on a
     // static grid is an OR (every free bit comes from clip(g,0,1)).
     const int rr = s.sq_r;
-    for (int idx = threadIdx.x; idx < N * We; idx += NT) {
+    for (int idx = C.sub; idx < N * We; idx += LPE) {
       const int a = udiv(idx, s.mg_We), r = idx - a * We;
       const int ox = L.x0[a] - H - 1, oy = L.y0[a] - H - 1;
       const int gx = ox + r, xa = L.x[a], ya = L.y[a];
@@ -388,9 +387,11 @@ __device__ __forceinline__ void sense(const State& s, const Lds<WT>& L) {
 }
 
 // single_square_tool: only the robot's own cell becomes free (:233-234)
-template <int NT, typename WT>
-__device__ __forceinline__ void single_tool(const State& s, const Lds<WT>& L) {
-  for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  for (int idx = C.sub; idx < s.N * s.We; idx += LPE) {
     const int a = udiv(idx, s.mg_We), r = idx - a * s.We;
     const int ox = L.x0[a] - s.H - 1, oy = L.y0[a] - s.H - 1;
     L.fp[idx] = (ox + r == L.x[a]) ? ((WT)1 << (L.y[a] - oy)) : (WT)0;
@@ -402,14 +403,21 @@ __device__ __forceinline__ void single_tool(const State& s, const Lds<WT>& L) {
 // union delta = cells some agent marked this step that were not yet visited,
 // each counted at the lowest-index agent that marked it.
 // --------------------------------------------------------------------------
-template <int NT, typename WT>
-__device__ __forceinline__ void merge(const State& s, const Lds<WT>& L, Items<WT>& I, const Agents& A) {
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI, WT>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int items = s.N * s.We;
   const uint64_t wmask = low_mask(s.We);
+  // EPW == 1: agent j's pre-move origin in lane j of every wave, broadcast by
+  // v_readlane (N <= 64)
+  const int jw = (int)(threadIdx.x & 63);
+  const int jl = jw < s.N ? jw : 0;
+  const int ax0 = L.x0[jl], ay0 = L.y0[jl];
   uint32_t cf = 0, cv = 0;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
-    const int idx = threadIdx.x + k * NT;
+    const int idx = C.sub + k * LPE;
     I.nf[k] = I.no[k] = I.nu[k] = 0;
     if (idx < items) {
       const WT fp = L.fp[idx], op = L.op[idx];
@@ -418,15 +426,20 @@ __device__ __forceinline__ void merge(const State& s, const Lds<WT>& L, Items<WT
       cf += popc(I.nf[k]);
       const int a = I.a[k], gx = I.gx[k], oy = I.oy[k];
       WT cand = fp & ~(WT)(funnel(I.u0[k], I.u1[k], oy & 63) & wmask);
-      if (cand) {
-        for (int b = 0; b < s.N; ++b) {  // marks of lower-index agents at these cells
-          const int xb = rdlane(A.x0, b), yb = rdlane(A.y0, b);
-          const int rb = gx - (xb - s.H - 1);
-          const int d = (yb - s.H - 1) - oy;  // column shift b -> a (|d| < We to overlap)
-          if (b < a && (unsigned)rb < (unsigned)s.We && d > -s.We && d < s.We) {
-            const WT pb = L.fp[b * s.We + rb];
-            cand &= ~(d >= 0 ? (pb << d) : (pb >> -d));
-          }
+      for (int b = 0; b < a; ++b) {  // marks of lower-index agents at these cells
+        int xb, yb;
+        if constexpr (EPW == 1) {
+          xb = rdlane(ax0, b);
+          yb = rdlane(ay0, b);
+        } else {
+          xb = L.x0[b];
+          yb = L.y0[b];
+        }
+        const int rb = gx - (xb - s.H - 1);
+        const int d = (yb - s.H - 1) - oy;  // column shift b -> a (|d| < We to overlap)
+        if ((unsigned)rb < (unsigned)s.We && d > -s.We && d < s.We) {
+          const WT pb = L.fp[b * s.We + rb];
+          cand &= ~(d >= 0 ? (WT)(pb << d) : (WT)(pb >> -d));
         }
       }
       I.nu[k] = cand;
@@ -438,28 +451,31 @@ __device__ __forceinline__ void merge(const State& s, const Lds<WT>& L, Items<WT
 }
 
 // after merge: fold |= fp (obs crops read the post-step maps)
-template <int NT, typename WT>
-__device__ __forceinline__ void fold_marks(const State& s, const Lds<WT>& L) {
-  for (int idx = threadIdx.x; idx < s.N * s.We; idx += NT) {
-    L.fold[idx] |= L.fp[idx];
-    L.oold[idx] |= L.op[idx];
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void fold_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  for (int idx = C.sub; idx < s.N * s.We; idx += LPE) {
+    C.L.fold[idx] |= C.L.fp[idx];
+    C.L.oold[idx] |= C.L.op[idx];
   }
 }
 
-template <int NT, typename WT>
-__device__ __forceinline__ void store_words(const State& s, int e, const Items<WT>& I) {
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void store_words(const State& s, const Ctx<NT, EPW, WT>& C,
+                                            const Items<KI, WT>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const int items = s.N * s.We;
   const size_t mw = (size_t)s.Wp * s.nw;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
-    const int idx = threadIdx.x + k * NT;
+    const int idx = C.sub + k * LPE;
     if (idx >= items) continue;
     const int gx = I.gx[k], oy = I.oy[k];
     if (!row_in(s, gx)) continue;
     const int w0 = oy >> 6, off = oy & 63;
     const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
     const size_t rb = (size_t)gx * s.nw;
-    const size_t fb = ((size_t)e * s.N + I.a[k]) * mw + rb;
+    const size_t fb = ((size_t)C.e * s.N + I.a[k]) * mw + rb;
     const uint64_t nf = I.nf[k], no = I.no[k], nu = I.nu[k];  // widened to the HBM word
     if (nf) {
       if (in0) s.freem[fb + w0] = I.f0[k] | (nf << off);
@@ -470,7 +486,7 @@ __device__ __forceinline__ void store_words(const State& s, int e, const Items<W
       if (in1) s.obstm[fb + w0 + 1] = I.o1[k] | (no >> (64 - off));
     }
     if (nu) {  // agents' windows overlap: several lanes may add bits to one word
-      unsigned long long* v = (unsigned long long*)(s.vis + (size_t)e * mw + rb);
+      unsigned long long* v = (unsigned long long*)(s.vis + (size_t)C.e * mw + rb);
       if (in0 && (nu << off)) atomicOr(v + w0, nu << off);
       if (in1 && (nu >> (64 - off))) atomicOr(v + w0 + 1, nu >> (64 - off));
     }
@@ -478,15 +494,20 @@ __device__ __forceinline__ void store_words(const State& s, int e, const Items<W
 }
 
 // --------------------------------------------------------------------------
-// reset (dec_grid_rl.py:449-531) of env e inside the launch: grid pick, start
-// cells (injected, or Philox rejection draw with the reference's acceptance
-// rule, :491-502), zeroed maps, initial observe() (reward discarded, :524).
+// reset (dec_grid_rl.py:449-531) of the slot's env inside the launch: grid
+// pick, start cells (injected, or Philox rejection draw with the reference's
+// acceptance rule, :491-502), zeroed maps, initial observe() (reward
+// discarded, :524).
 // --------------------------------------------------------------------------
-template <int NT, typename WT>
-__device__ __forceinline__ void reset_env(const State& s, const Lds<WT>& L, int e, const int32_t* inj_pos) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
+                                          const int32_t* inj_pos) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int KI = Ctx<NT, EPW, WT>::KI;
+  const Lds<WT>& L = C.L;
   const int N = s.N;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
+  const int e = C.e;
+  if (C.sub == 0) {
     const uint32_t ep = s.episode[e] + 1u;
     s.episode[e] = ep;
     L.sc->ep = ep;
@@ -507,37 +528,39 @@ __device__ __forceinline__ void reset_env(const State& s, const Lds<WT>& L, int 
   {  // zero this env's maps (:505-514)
     uint64_t* f = s.freem + (size_t)e * N * mw;
     uint64_t* o = s.obstm + (size_t)e * N * mw;
-    for (size_t i = tid; i < (size_t)N * mw; i += NT) { f[i] = 0; o[i] = 0; }
+    for (size_t i = C.sub; i < (size_t)N * mw; i += LPE) { f[i] = 0; o[i] = 0; }
     uint64_t* v = s.vis + (size_t)e * mw;
-    for (size_t i = tid; i < mw; i += NT) v[i] = 0;
+    for (size_t i = C.sub; i < mw; i += LPE) v[i] = 0;
   }
   if (inj_pos != nullptr) {
-    if (tid < N) {
-      const int x = inj_pos[((size_t)e * N + tid) * 2];
-      const int y = inj_pos[((size_t)e * N + tid) * 2 + 1];
+    if (C.sub < N) {
+      const int x = inj_pos[((size_t)e * N + C.sub) * 2];
+      const int y = inj_pos[((size_t)e * N + C.sub) * 2 + 1];
       bool bad = grid_blocked(s, g, x, y);
-      for (int j = 0; j < tid; ++j)
+      for (int j = 0; j < C.sub; ++j)
         bad |= (inj_pos[((size_t)e * N + j) * 2] == x && inj_pos[((size_t)e * N + j) * 2 + 1] == y);
       if (bad) atomicOr(s.err, ERR_INJECT);
-      L.x0[tid] = L.x[tid] = x;
-      L.y0[tid] = L.y[tid] = y;
+      L.x0[C.sub] = L.x[C.sub] = x;
+      L.y0[C.sub] = L.y[C.sub] = y;
     }
-  } else if (tid < 64) {
+  } else if (C.sub < 64) {
     // x = randint(W), y = randint(L); accept iff grid >= 0 and unoccupied;
-    // candidates are consumed strictly in draw order
-    const int lane = tid;
+    // candidates (Philox counter = candidate index) are consumed strictly in
+    // draw order, CPR of them per round
+    const int lane = C.sub;
+    constexpr int CPR = LPE < 64 ? LPE : 64;
     int px = INT32_MIN / 2, py = INT32_MIN / 2, placed = 0;
-    for (int round = 0; round < 256 && placed < N; ++round) {
-      const uint32_t k = (uint32_t)(round * 64 + lane);
+    for (int round = 0; round < 1024 && placed < N; ++round) {
+      const uint32_t k = (uint32_t)(round * CPR + lane);
       const uint4 r = philox(s.seed, make_uint4(k, (uint32_t)e, ep, 0x706c6163u));
       const int cx = (int)bounded(r.x, (uint32_t)s.Wp);
       const int cy = (int)bounded(r.y, (uint32_t)s.Lp);
-      uint64_t okm = __ballot(!grid_blocked(s, g, cx, cy));
+      uint64_t okm = slot_ballot(C, !grid_blocked(s, g, cx, cy));
       while (okm && placed < N) {
         const int j = __ffsll((unsigned long long)okm) - 1;
         okm &= okm - 1;
-        const int qx = rdlane(cx, j), qy = rdlane(cy, j);
-        const bool clash = __ballot(lane < placed && px == qx && py == qy) != 0ull;
+        const int qx = bcast(C, cx, j), qy = bcast(C, cy, j);
+        const bool clash = slot_ballot(C, lane < placed && px == qx && py == qy) != 0ull;
         if (!clash) {
           if (lane == placed) { px = qx; py = qy; }
           ++placed;
@@ -553,21 +576,18 @@ __device__ __forceinline__ void reset_env(const State& s, const Lds<WT>& L, int 
   // the zeroing stores must land before the window stores / atomics below
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  Items<WT> I;
-  stage<NT, WT>(s, L, e, /*load_masks=*/false, I);
+  Items<KI, WT> I;
+  stage<NT, EPW, WT, KI>(s, C, /*load_masks=*/false, I);
   __syncthreads();
-  sense<NT, WT>(s, L);
+  sense<NT, EPW, WT>(s, C);
   __syncthreads();
-  if (s.sst) { single_tool<NT, WT>(s, L); __syncthreads(); }
-  {
-    const Agents A = load_agents<WT>(s, L);
-    merge<NT, WT>(s, L, I, A);
-  }
+  if (s.sst) { single_tool<NT, EPW, WT>(s, C); __syncthreads(); }
+  merge<NT, EPW, WT, KI>(s, C, I);
   __syncthreads();
-  fold_marks<NT, WT>(s, L);
-  store_words<NT, WT>(s, e, I);
+  fold_marks<NT, EPW, WT>(s, C);
+  store_words<NT, EPW, WT, KI>(s, C, I);
   __syncthreads();
-  if (tid == 0) {
+  if (C.sub == 0) {
     s.free_cnt[e] = L.sc->cnt_free;
     s.vis_cnt[e] = L.sc->cnt_vis;
     s.currstep[e] = 0;
@@ -579,13 +599,14 @@ __device__ __forceinline__ void reset_env(const State& s, const Lds<WT>& L, int 
 // E x E around each robot.  Each (agent, layer, row) becomes one E-bit byte
 // in LDS; the uint8 output is then written as dwords.
 // --------------------------------------------------------------------------
-template <int NT, typename WT>
-__device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int e, uint8_t* obs_out) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>& C, uint8_t* obs_out) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc, H = s.H;
   const uint64_t moved = L.sc->moved;
   const WT emask = wmask_of<WT>(E);
-  const Agents A = load_agents<WT>(s, L);
-  for (int idx = threadIdx.x; idx < N * Lc * E; idx += NT) {
+  for (int idx = C.sub; idx < N * Lc * E; idx += LPE) {
     const int a = udiv(idx, s.mg_LcE), rem = idx - a * (Lc * E);
     const int layer = udiv(rem, s.mg_E), r = rem - layer * E;
     const int xa = L.x[a], ya = L.y[a];
@@ -594,8 +615,8 @@ __device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int 
       const int cx = xa - ego + r, cy0 = ya - ego;
       for (uint64_t m = moved; m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
-        const int dc = rdlane(A.y, j) - cy0;
-        if (rdlane(A.x, j) == cx && dc >= 0 && dc < E) bits |= (WT)1 << dc;
+        const int dc = L.y[j] - cy0;
+        if (L.x[j] == cx && dc >= 0 && dc < E) bits |= (WT)1 << dc;
       }
     } else if (layer <= 2) {
       const int er = xa - ego + r - (L.x0[a] - H - 1);
@@ -607,10 +628,10 @@ __device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int 
   }
   __syncthreads();
   const int total = N * Lc * E * E;
-  uint8_t* dst = obs_out + (size_t)e * total;
+  uint8_t* dst = obs_out + (size_t)C.e * total;
   if ((total & 3) == 0) {
     uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-    for (int i = threadIdx.x; i < total / 4; i += NT) {
+    for (int i = C.sub; i < total / 4; i += LPE) {
       uint32_t v = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -621,7 +642,7 @@ __device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int 
       d32[i] = v;
     }
   } else {
-    for (int q = threadIdx.x; q < total; q += NT) {
+    for (int q = C.sub; q < total; q += LPE) {
       const int row = udiv(q, s.mg_E), col = q - row * E;
       dst[q] = (uint8_t)((L.obsrow[row] >> col) & 1);
     }
@@ -629,9 +650,9 @@ __device__ __forceinline__ void write_obs(const State& s, const Lds<WT>& L, int 
 }
 
 // --------------------------------------------------------------------------
-// the env kernel: one workgroup per env
+// the env kernel: EPW envs per workgroup
 // --------------------------------------------------------------------------
-template <int NT, typename WT>
+template <int NT, int EPW, typename WT>
 __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ env_mask,
                                                  const int32_t* __restrict__ inj_pos,
@@ -639,26 +660,39 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
                                                  uint8_t* __restrict__ done_out,
                                                  uint8_t* __restrict__ obs_out,
                                                  uint8_t* __restrict__ adj_out) {
+  using CtxT = Ctx<NT, EPW, WT>;
+  constexpr int LPE = CtxT::LPE;
+  constexpr int KI = CtxT::KI;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int e = blockIdx.x;
   const int tid = threadIdx.x;
   const int N = s.N;
-  const Lds<WT> L = carve<WT>(smem, s);
+  CtxT C;
+  const int slot = EPW == 1 ? 0 : tid / LPE;
+  C.sub = EPW == 1 ? tid : tid - slot * LPE;
+  C.lane0 = EPW == 1 ? 0 : slot * LPE;
+  const int e_raw = blockIdx.x * EPW + slot;
+  const bool valid = e_raw < s.B;  // a short last workgroup leaves a slot idle
+  C.e = valid ? e_raw : s.B - 1;
+  const size_t slot_lds =
+      env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E, sizeof(WT));
+  C.L = carve<WT>(smem + slot * slot_lds, s);
+  const Lds<WT>& L = C.L;
+  const int e = C.e;
 
   const bool is_step = mode == MODE_STEP;
-  const bool sentinel = is_step && actions[(size_t)e * N] == 255;
-  const bool reset_req = !is_step && (env_mask == nullptr || env_mask[e] != 0);
-  const bool active = is_step && !sentinel;
+  const bool sentinel = valid && is_step && actions[(size_t)e * N] == 255;
+  const bool reset_req = valid && !is_step && (env_mask == nullptr || env_mask[e] != 0);
+  const bool active = valid && is_step && !sentinel;
 
   STAMP(0);
   // ---- round trip 1: positions, actions, scalars, beam table ---------------
-  if (tid < N) {
-    const int2 p = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + tid];
-    L.x0[tid] = L.x[tid] = p.x;
-    L.y0[tid] = L.y[tid] = p.y;
-    if (active) L.act[tid] = actions[(size_t)e * N + tid];
+  if (C.sub < N) {
+    const int2 p = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + C.sub];
+    L.x0[C.sub] = L.x[C.sub] = p.x;
+    L.y0[C.sub] = L.y[C.sub] = p.y;
+    if (active) L.act[C.sub] = actions[(size_t)e * N + C.sub];
   }
-  if (tid == 0) {
+  if (C.sub == 0) {
     const int g = s.env_grid[e];
     L.sc->grid = g;
     L.sc->moved = s.moved[e];
@@ -674,30 +708,27 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     }
   }
   if (s.sensor == 0)
-    for (int b = tid; b < s.nbeams; b += NT) L.beams[b] = s.beams[b];
+    for (int b = C.sub; b < s.nbeams; b += LPE) L.beams[b] = s.beams[b];
   __syncthreads();
 
   if (active) {
     STAMP(1);
-    Items<WT> I;
-    stage<NT, WT>(s, L, e, true, I);  // ---- round trip 2 ----
-    if (tid == 0) L.sc->numfree = s.numfree[L.sc->grid];
+    Items<KI, WT> I;
+    stage<NT, EPW, WT, KI>(s, C, true, I);  // ---- round trip 2 ----
+    if (C.sub == 0) L.sc->numfree = s.numfree[L.sc->grid];
     __syncthreads();
     STAMP(2);
-    if (tid < 64) moves<WT>(s, L, -s.pen);
+    if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
     __syncthreads();
     STAMP(3);
-    sense<NT, WT>(s, L);
+    sense<NT, EPW, WT>(s, C);
     __syncthreads();
     STAMP(4);
-    if (s.sst) { single_tool<NT, WT>(s, L); __syncthreads(); }
-    {
-      const Agents A = load_agents<WT>(s, L);
-      merge<NT, WT>(s, L, I, A);
-    }
+    if (s.sst) { single_tool<NT, EPW, WT>(s, C); __syncthreads(); }
+    merge<NT, EPW, WT, KI>(s, C, I);
     __syncthreads();
     STAMP(5);
-    if (tid == 0) {
+    if (C.sub == 0) {
       Scal* c = L.sc;
       const uint32_t fc = c->free_old + c->cnt_free;
       const uint32_t vc = c->vis_old + c->cnt_vis;
@@ -723,20 +754,20 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     __syncthreads();
     STAMP(6);
     if (!L.sc->do_reset) {
-      fold_marks<NT, WT>(s, L);
-      store_words<NT, WT>(s, e, I);
+      fold_marks<NT, EPW, WT>(s, C);
+      store_words<NT, EPW, WT, KI>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, WT>(s, L, e, nullptr);  // the finished episode's words are not stored
+      reset_env<NT, EPW, WT>(s, C, nullptr);  // the finished episode's words are not stored
     }
   } else if (reset_req) {
-    reset_env<NT, WT>(s, L, e, inj_pos);
+    reset_env<NT, EPW, WT>(s, C, inj_pos);
   } else {
     // sentinel step / env left out of a partial reset: obs of the current
     // state only (dec_grid_rl.py:104-107,160)
-    Items<WT> I;
-    stage<NT, WT>(s, L, e, true, I);
-    if (tid == 0 && sentinel) {
+    Items<KI, WT> I;
+    stage<NT, EPW, WT, KI>(s, C, true, I);
+    if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
     }
@@ -744,17 +775,16 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
   __syncthreads();
 
   if (active || reset_req) {
-    if (tid < N) {
-      reinterpret_cast<int2*>(s.pos)[(size_t)e * N + tid] = make_int2(L.x[tid], L.y[tid]);
-    }
-    if (tid == 0) s.moved[e] = L.sc->moved;
+    if (C.sub < N)
+      reinterpret_cast<int2*>(s.pos)[(size_t)e * N + C.sub] = make_int2(L.x[C.sub], L.y[C.sub]);
+    if (C.sub == 0) s.moved[e] = L.sc->moved;
   }
   STAMP(8);
-  write_obs<NT, WT>(s, L, e, obs_out);
+  if (valid) write_obs<NT, EPW, WT>(s, C, obs_out);
   STAMP(9);
-  if (adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
+  if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
     uint8_t* ad = adj_out + (size_t)e * N * N;
-    for (int idx = tid; idx < N * N; idx += NT) {
+    for (int idx = C.sub; idx < N * N; idx += LPE) {
       const int i = idx / N, j = idx - i * N;
       const int dx = abs(L.x[i] - L.x[j]), dy = abs(L.y[i] - L.y[j]);
       ad[idx] = (max(dx, dy) <= s.comm_r) ? 1 : 0;
@@ -766,31 +796,42 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
   STAMP(10);
 }
 
+// Envs per wave: two when an env fits 32 lanes (N <= 32, at most 3 staged
+// rows and 3 beams per lane), else one env per workgroup of NT threads.
+int env_pack(const State& s) {
+  const int items = s.N * s.We;
+  const int rays = s.sensor == 0 ? s.N * s.nbeams : 0;
+  return (s.N <= 32 && items <= 3 * 32 && rays <= 3 * 32) ? 2 : 1;
+}
+
 hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
-                      uint8_t* adj, int nt, hipStream_t stream) {
+                      uint8_t* adj, int nt, int epw, hipStream_t stream) {
   const bool narrow = s.We <= 32;
-  const size_t lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
-                                   narrow ? 4 : 8);
-  dim3 grid(s.B), block(nt);
-#define MC_LAUNCH(T, W)                                                                          \
-  hipLaunchKernelGGL((env_kernel<T, W>), grid, block, lds, stream, s, mode, actions, env_mask, \
-                     inj_pos, reward, done, obs, adj)
-  if (narrow) {
+  const size_t slot_lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
+                                        narrow ? 4 : 8);
+#define MC_LAUNCH(T, P, W)                                                                     \
+  hipLaunchKernelGGL((env_kernel<T, P, W>), dim3((s.B + (P)-1) / (P)), dim3(T),               \
+                     slot_lds * (P), stream, s, mode, actions, env_mask, inj_pos, reward, done, \
+                     obs, adj)
+  if (epw == 2) {
+    if (narrow) MC_LAUNCH(64, 2, uint32_t);
+    else MC_LAUNCH(64, 2, uint64_t);
+  } else if (narrow) {
     switch (nt) {
-      case 64: MC_LAUNCH(64, uint32_t); break;
-      case 128: MC_LAUNCH(128, uint32_t); break;
-      case 256: MC_LAUNCH(256, uint32_t); break;
-      case 512: MC_LAUNCH(512, uint32_t); break;
-      default: MC_LAUNCH(1024, uint32_t); break;
+      case 64: MC_LAUNCH(64, 1, uint32_t); break;
+      case 128: MC_LAUNCH(128, 1, uint32_t); break;
+      case 256: MC_LAUNCH(256, 1, uint32_t); break;
+      case 512: MC_LAUNCH(512, 1, uint32_t); break;
+      default: MC_LAUNCH(1024, 1, uint32_t); break;
     }
   } else {
     switch (nt) {
-      case 64: MC_LAUNCH(64, uint64_t); break;
-      case 128: MC_LAUNCH(128, uint64_t); break;
-      case 256: MC_LAUNCH(256, uint64_t); break;
-      case 512: MC_LAUNCH(512, uint64_t); break;
-      default: MC_LAUNCH(1024, uint64_t); break;
+      case 64: MC_LAUNCH(64, 1, uint64_t); break;
+      case 128: MC_LAUNCH(128, 1, uint64_t); break;
+      case 256: MC_LAUNCH(256, 1, uint64_t); break;
+      case 512: MC_LAUNCH(512, 1, uint64_t); break;
+      default: MC_LAUNCH(1024, 1, uint64_t); break;
     }
   }
 #undef MC_LAUNCH
