@@ -83,6 +83,7 @@ struct Lds {
   Scal* sc;
   uint8_t* act;
   uint8_t* obsrow;  // [N*Lc*E] E-bit crop rows
+  WT* sink;         // [64] target of lidar marks a lane does not make
 };
 
 template <typename WT>
@@ -109,6 +110,8 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   L.act = reinterpret_cast<uint8_t*>(q);
   q += ((size_t)s.N + 15) & ~(size_t)15;
   L.obsrow = reinterpret_cast<uint8_t*>(q);
+  q += ((size_t)s.N * s.Lc * s.E + 15) & ~(size_t)15;
+  L.sink = reinterpret_cast<WT*>(q);
   return L;
 }
 
@@ -310,17 +313,24 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
 }
 
 __device__ __forceinline__ void ray_advance(Ray& R, int k) {
-  const int mv = (int)((R.bits >> k) & 1u);
-  R.row += R.drow + mv * R.mrow;
-  R.col += R.dcol + mv * R.mcol;
+  const bool mv = (R.bits >> k) & 1u;
+  R.row += R.drow + (mv ? R.mrow : 0);
+  R.col += R.dcol + (mv ? R.mcol : 0);
 }
 
+// Branch-free mark: every lane issues one ds_or per ray and step; a lane with
+// nothing to mark ORs into its own sink word (no bank conflicts, no exec-mask
+// branches).  Re-marking an already free cell is harmless (OR).
 template <typename WT>
-__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow) {
+__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT* sink) {
   const bool on = R.live && k <= R.K;
   const WT bit = (WT)1 << R.col;
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
-  if (on && (hit || !(frow & bit))) lds_or((hit ? L.op : L.fp) + R.row, bit);
+#if defined(MC_ABL) && MC_ABL == 1
+  lds_or(sink, bit);  // timing ablation: no marks
+#else
+  lds_or(on ? (hit ? L.op : L.fp) + R.row : sink, bit);
+#endif
   R.live = on && !hit;
 }
 
@@ -337,25 +347,27 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
       lds_or(&L.fp[a * We + r0], (WT)1 << c0);
     }
     const int total = N * s.nbeams;
-    for (int base = C.sub; base < total; base += RPL * LPE) {
+    // lane l of a pass takes rays RPL*l .. RPL*l+RPL-1: within one ds_or the
+    // lanes of an agent hold beams RPL apart, which mostly land in different
+    // rows (fewer same-address LDS atomics than adjacent beams)
+    for (int base = C.sub * RPL; base < total; base += RPL * LPE) {
       Ray q[RPL];
-      int kmax = 0;
 #pragma unroll
       for (int j = 0; j < RPL; ++j) {
-        q[j] = ray_init<WT>(s, L, base + j * LPE);
+        q[j] = ray_init<WT>(s, L, base + j);
         ray_advance(q[j], 0);
-        kmax = max(kmax, q[j].K);
       }
+      // wave-uniform trip count (every cell with k <= K <= beam_kmax <= H
+      // lies inside the staged window)
+      const int kmax = s.beam_kmax;
+      WT* sink = L.sink + (threadIdx.x & 63);
       for (int k = 1; k <= kmax; ++k) {
-        WT nr[RPL], fr[RPL];
+        WT nr[RPL];
 #pragma unroll
-        for (int j = 0; j < RPL; ++j) {  // all row reads of this step in flight
-          nr[j] = L.neg[q[j].row];
-          fr[j] = L.fp[q[j].row];
-        }
+        for (int j = 0; j < RPL; ++j) nr[j] = L.neg[q[j].row];  // all row reads in flight
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
-          ray_mark<WT>(L, q[j], k, nr[j], fr[j]);
+          ray_mark<WT>(L, q[j], k, nr[j], sink);
           ray_advance(q[j], k);
         }
       }
@@ -426,7 +438,11 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       cf += popc(I.nf[k]);
       const int a = I.a[k], gx = I.gx[k], oy = I.oy[k];
       WT cand = fp & ~(WT)(funnel(I.u0[k], I.u1[k], oy & 63) & wmask);
+#if defined(MC_ABL) && MC_ABL == 4
+      for (int b = 0; b < 0; ++b) {  // timing ablation: no dedup
+#else
       for (int b = 0; b < a; ++b) {  // marks of lower-index agents at these cells
+#endif
         int xb, yb;
         if constexpr (EPW == 1) {
           xb = rdlane(ax0, b);
@@ -721,7 +737,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
     __syncthreads();
     STAMP(3);
+#if !(defined(MC_ABL) && MC_ABL == 3)
     sense<NT, EPW, WT>(s, C);
+#endif
     __syncthreads();
     STAMP(4);
     if (s.sst) { single_tool<NT, EPW, WT>(s, C); __syncthreads(); }
@@ -780,7 +798,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
     if (C.sub == 0) s.moved[e] = L.sc->moved;
   }
   STAMP(8);
+#if !(defined(MC_ABL) && MC_ABL == 5)
   if (valid) write_obs<NT, EPW, WT>(s, C, obs_out);
+#endif
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
     uint8_t* ad = adj_out + (size_t)e * N * N;

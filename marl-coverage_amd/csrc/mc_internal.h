@@ -59,6 +59,7 @@ struct State {
   const Beam* beams;
   const uint64_t* beam_bits;  // [nbeams][bcmax] minor-move bits per start coordinate
   int bcmax;                  // max(Wp, Lp)
+  int beam_kmax;              // max Beam::K (<= H): march steps of a pass
   int32_t* env_grid;
   int32_t* pos;
   uint64_t* moved;
@@ -90,7 +91,9 @@ __host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int L
   b += 64;                                   // scalars
   b += ((size_t)N + 15) & ~(size_t)15;       // actions
   b += (((size_t)N * Lc * E) + 15) & ~(size_t)15;  // obs rows (one E-bit byte each)
-  return (b + 15) & ~(size_t)15;
+  b = (b + 15) & ~(size_t)15;
+  b += 64 * wbytes;  // per-lane sink word for masked-off lidar marks
+  return b;
 }
 
 }  // namespace mc

@@ -15,6 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "marl-coverage_amd")
 LIB = os.path.join(PKG, "libmarlcov_stamps.so")
+# MC_ABL timing ablations (wrong results): 1 sense without marks, 2 sense
+# without the skip test, 3 no sense, 4 merge without dedup, 5 no obs
+ABLATIONS = (1, 2, 3, 4, 5)
 PHASES = ["rt1 pos/act/scalars", "rt2 stage", "moves", "sense", "merge", "reward",
           "store", "(reset)", "obs", "adj+drain"]
 
@@ -35,12 +38,12 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--abl", type=int, default=None, help="timing ablation build (wrong results)")
-    ap.add_argument("--all-abl", action="store_true", help="also build ablations 1..3")
+    ap.add_argument("--all-abl", action="store_true", help="also build ablations 1..5")
     args = ap.parse_args()
     if args.build_only or not os.path.exists(LIB):
         build()
         if args.all_abl:
-            for a in (1, 2, 3):
+            for a in ABLATIONS:
                 build(a)
         if args.build_only:
             return
@@ -65,9 +68,18 @@ def main():
         env.step(a)
     torch.cuda.synchronize()
     s = st.cpu().numpy().astype(np.int64)
+    s = s[s[:, 0] > 0]  # one stamp row per workgroup (first env slot)
     t0 = s[:, 0].min()
     print(f"envs={B}  wave start spread (cycles): median {np.median(s[:,0]-t0):.0f}  max {(s[:,0]-t0).max()}")
     print(f"kernel span (first start -> last end): {s[:,10].max()-t0} cycles")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    acts = torch.randint(0, 4, (20, B, 4), dtype=torch.uint8, device=env.device)
+    ev0.record()
+    for t in range(20):
+        env.step(acts[t])
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"eager step (stamped build): {ev0.elapsed_time(ev1) / 20 * 1000:.2f} us")
     order = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), (7, 8), (8, 9), (9, 10)]
     for (i, j), name in zip(order, PHASES):
         ok = (s[:, i] > 0) & (s[:, j] > 0)
