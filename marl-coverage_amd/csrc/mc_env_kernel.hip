@@ -730,7 +730,11 @@ __global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_
   if (active) {
     STAMP(1);
     Items<KI, WT> I;
+#if defined(MC_ABL) && MC_ABL == 6
+    stage<NT, EPW, WT, KI>(s, C, false, I);  // timing ablation: grid words only
+#else
     stage<NT, EPW, WT, KI>(s, C, true, I);  // ---- round trip 2 ----
+#endif
     if (C.sub == 0) L.sc->numfree = s.numfree[L.sc->grid];
     __syncthreads();
     STAMP(2);
