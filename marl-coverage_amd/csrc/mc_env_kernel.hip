@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "mc_device.h"
+#include <cstdlib>
 
 namespace mc {
 
@@ -177,47 +178,73 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   const uint64_t wmask = low_mask(s.We);
   const bool square = s.sensor == 1;
   uint64_t n0[KI], n1[KI], p0[KI], p1[KI];
+  // addresses first, then every load of the lane back to back with no
+  // exec-mask branches (words outside the grid read index 0 and are
+  // replaced below), so the whole stage is one memory round trip
+  size_t i0[KI], i1[KI], fb[KI];
+  bool in0[KI], in1[KI];
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const int idx = C.sub + k * LPE;
-    n0[k] = n1[k] = ~0ull;
-    p0[k] = p1[k] = 0;
-    I.f0[k] = I.f1[k] = I.o0[k] = I.o1[k] = I.u0[k] = I.u1[k] = 0;
-    I.a[k] = 0;
-    I.gx[k] = -1;
-    I.oy[k] = 0;
-    if (idx < items) {
-      const int a = udiv(idx, s.mg_We);
-      const int r = idx - a * s.We;
-      const int gx = L.x0[a] - s.H - 1 + r;
-      const int oy = L.y0[a] - s.H - 1;
-      I.a[k] = a;
-      I.gx[k] = gx;
-      I.oy[k] = oy;
-      const int w0 = oy >> 6;
-      const bool in0 = word0_in(s, gx, oy), in1 = word1_in(s, gx, oy);
-      const size_t rb = (size_t)(row_in(s, gx) ? gx : 0) * s.nw;
-      const size_t fb = ((size_t)C.e * s.N + a) * mw + rb;
-      const size_t vb = (size_t)C.e * mw + rb;
-      if (in0) {
-        n0[k] = gn[rb + w0];
-        if (square) p0[k] = gp[rb + w0];
-        if (load_masks) {
-          I.f0[k] = s.freem[fb + w0];
-          I.o0[k] = s.obstm[fb + w0];
-          I.u0[k] = s.vis[vb + w0];
-        }
-      }
-      if (in1) {
-        n1[k] = gn[rb + w0 + 1];
-        if (square) p1[k] = gp[rb + w0 + 1];
-        if (load_masks) {
-          I.f1[k] = s.freem[fb + w0 + 1];
-          I.o1[k] = s.obstm[fb + w0 + 1];
-          I.u1[k] = s.vis[vb + w0 + 1];
-        }
-      }
+    const bool it = idx < items;
+    const int a = it ? udiv(idx, s.mg_We) : 0;
+    const int r = idx - a * s.We;
+    const int gx = L.x0[a] - s.H - 1 + r;
+    const int oy = L.y0[a] - s.H - 1;
+    I.a[k] = a;
+    I.gx[k] = it ? gx : -1;
+    I.oy[k] = oy;
+    const int w0 = oy >> 6;
+    in0[k] = it && word0_in(s, gx, oy);
+    in1[k] = it && word1_in(s, gx, oy);
+    const size_t rb = (size_t)(row_in(s, gx) ? gx : 0) * s.nw;
+#if defined(MC_ABL) && MC_ABL == 7
+    // timing ablation: word-planar addresses (word w of row x at w*Wp + x)
+    i0[k] = in0[k] ? (size_t)w0 * s.Wp + (rb / s.nw) : 0;
+    i1[k] = in1[k] ? (size_t)(w0 + 1) * s.Wp + (rb / s.nw) : 0;
+#else
+    i0[k] = in0[k] ? rb + w0 : 0;
+    i1[k] = in1[k] ? rb + w0 + 1 : 0;
+#endif
+    fb[k] = ((size_t)C.e * s.N + a) * mw;
+  }
+  const size_t vb = (size_t)C.e * mw;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    n0[k] = gn[i0[k]];
+    n1[k] = gn[i1[k]];
+    if (load_masks) {
+      I.f0[k] = s.freem[fb[k] + i0[k]];
+      I.f1[k] = s.freem[fb[k] + i1[k]];
+      I.o0[k] = s.obstm[fb[k] + i0[k]];
+      I.o1[k] = s.obstm[fb[k] + i1[k]];
+      I.u0[k] = s.vis[vb + i0[k]];
+      I.u1[k] = s.vis[vb + i1[k]];
     }
+    if (square) {
+      p0[k] = gp[i0[k]];
+      p1[k] = gp[i1[k]];
+    }
+  }
+#ifdef MC_STAMPS
+  STAMP(11);  // loads issued
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(12);  // loads landed
+#endif
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    // outside the grid: blocked (isInBounds), no marks
+    n0[k] = in0[k] ? n0[k] : ~0ull;
+    n1[k] = in1[k] ? n1[k] : ~0ull;
+    p0[k] = (square && in0[k]) ? p0[k] : 0;
+    p1[k] = (square && in1[k]) ? p1[k] : 0;
+    const bool m0 = load_masks && in0[k], m1 = load_masks && in1[k];
+    I.f0[k] = m0 ? I.f0[k] : 0;
+    I.o0[k] = m0 ? I.o0[k] : 0;
+    I.u0[k] = m0 ? I.u0[k] : 0;
+    I.f1[k] = m1 ? I.f1[k] : 0;
+    I.o1[k] = m1 ? I.o1[k] : 0;
+    I.u1[k] = m1 ? I.u1[k] : 0;
   }
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
@@ -668,14 +695,16 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>
 // --------------------------------------------------------------------------
 // the env kernel: EPW envs per workgroup
 // --------------------------------------------------------------------------
-template <int NT, int EPW, typename WT>
-__global__ __launch_bounds__(NT) void env_kernel(State s, int mode, const uint8_t* __restrict__ actions,
+template <int NT, int EPW, typename WT, class SH>
+__global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ env_mask,
                                                  const int32_t* __restrict__ inj_pos,
                                                  double* __restrict__ reward_out,
                                                  uint8_t* __restrict__ done_out,
                                                  uint8_t* __restrict__ obs_out,
                                                  uint8_t* __restrict__ adj_out) {
+  State s = s_in;
+  specialize<SH>(s);
   using CtxT = Ctx<NT, EPW, WT>;
   constexpr int LPE = CtxT::LPE;
   constexpr int KI = CtxT::KI;
@@ -828,18 +857,32 @@ int env_pack(const State& s) {
   return (s.N <= 32 && items <= 3 * 32 && rays <= 3 * 32) ? 2 : 1;
 }
 
+// MARLCOV_SPECIALIZE=0 forces the generic (runtime-shape) kernels (A/B tests)
+static bool getenv_spec() {
+  static const bool on = [] {
+    const char* v = getenv("MARLCOV_SPECIALIZE");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
                       uint8_t* adj, int nt, int epw, hipStream_t stream) {
   const bool narrow = s.We <= 32;
   const size_t slot_lds = env_lds_bytes(s.N, s.We, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
                                         narrow ? 4 : 8);
-#define MC_LAUNCH(T, P, W)                                                                     \
-  hipLaunchKernelGGL((env_kernel<T, P, W>), dim3((s.B + (P)-1) / (P)), dim3(T),               \
-                     slot_lds * (P), stream, s, mode, actions, env_mask, inj_pos, reward, done, \
+#define MC_LAUNCH_SH(T, P, W, SH)                                                               \
+  hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + (P)-1) / (P)), dim3(T),              \
+                     slot_lds * (P), stream, s, mode, actions, env_mask, inj_pos, reward, done,    \
                      obs, adj)
+#define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
+  using Dynamic = Shape<0, 0, 0, 0, 0>;
+  using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
+  const bool spec_ok = getenv_spec();
   if (epw == 2) {
-    if (narrow) MC_LAUNCH(64, 2, uint32_t);
+    if (narrow && spec_ok && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
+    else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
   } else if (narrow) {
     switch (nt) {
@@ -858,6 +901,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
       default: MC_LAUNCH(1024, 1, uint64_t); break;
     }
   }
+#undef MC_LAUNCH_SH
 #undef MC_LAUNCH
   return hipGetLastError();
 }

@@ -79,7 +79,19 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, row) items per lane
 
 // floor(n / d) == umulhi(n, magic(d)) for 2 <= d < 2^16 and n * d < 2^32;
 // d == 1 (2^32 does not fit) is encoded as 0 and handled by the caller
-inline uint32_t magic_div(uint32_t d) { return d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d); }
+__host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
+  return d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d);
+}
+
+// Compile-time shape of an env kernel instantiation: fields > 0 are baked in
+// (loop bounds, divisions and LDS offsets fold to constants and the march
+// unrolls); 0 leaves the field to the runtime State.  The launcher picks a
+// specialised instantiation only when the runtime State matches it exactly.
+template <int N_, int H_, int NB_, int EGO_, int KM_>
+struct Shape {
+  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_;
+  __host__ __device__ static bool matches(const struct State& s);
+};
 
 // LDS bytes of the env kernel (host + device use the same carve).
 __host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int Lc, int E,
@@ -94,6 +106,37 @@ __host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int L
   b = (b + 15) & ~(size_t)15;
   b += 64 * wbytes;  // per-lane sink word for masked-off lidar marks
   return b;
+}
+
+template <int N_, int H_, int NB_, int EGO_, int KM_>
+__host__ __device__ inline bool Shape<N_, H_, NB_, EGO_, KM_>::matches(const State& s) {
+  return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
+         (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) && (EGO_ == 0 || s.ego == EGO_) &&
+         (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_));
+}
+
+// overwrite the baked-in fields of a kernel's State copy with constants
+template <class SH>
+__device__ __forceinline__ void specialize(State& s) {
+  if constexpr (SH::N > 0) s.N = SH::N;
+  if constexpr (SH::H > 0) {
+    s.H = SH::H;
+    s.We = 2 * SH::H + 3;
+    s.mg_We = magic_div(2 * SH::H + 3);
+  }
+  if constexpr (SH::NB > 0) {
+    s.sensor = 0;
+    s.nbeams = SH::NB;
+    s.mg_nb = magic_div(SH::NB);
+  }
+  if constexpr (SH::EGO > 0) {
+    s.ego = SH::EGO;
+    s.E = 2 * SH::EGO + 1;
+    s.Lc = 3;
+    s.mg_E = magic_div(2 * SH::EGO + 1);
+    s.mg_LcE = magic_div(3 * (2 * SH::EGO + 1));
+  }
+  if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
 }
 
 }  // namespace mc

@@ -11,3 +11,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HI
   timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/pmc_$n" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu --eager --steps 50 --warmup 5 > "$OUT/pmc_$n.log" 2>&1
   rc=$?; echo "pmc $n rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
+exit 0

@@ -16,8 +16,9 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "marl-coverage_amd")
 LIB = os.path.join(PKG, "libmarlcov_stamps.so")
 # MC_ABL timing ablations (wrong results): 1 lidar marks to the sink only,
-# 3 no sense, 4 merge without dedup, 5 no obs, 6 stage without the mask loads
-ABLATIONS = (1, 3, 4, 5, 6)
+# 3 no sense, 4 merge without dedup, 5 no obs, 6 stage without the mask loads,
+# 7 stage loads at word-planar addresses
+ABLATIONS = (1, 3, 4, 5, 6, 7)
 PHASES = ["rt1 pos/act/scalars", "rt2 stage", "moves", "sense", "merge", "reward",
           "store", "(reset)", "obs", "adj+drain"]
 
@@ -88,6 +89,11 @@ def main():
             continue
         d = s[ok, j] - s[ok, i]
         print(f"  {name:22s} median {np.median(d):8.0f}  p90 {np.percentile(d,90):8.0f}  max {d.max():8d}  n={ok.sum()}")
+    for (i, j), name in [((1, 11), "stage: issue"), ((11, 12), "stage: wait"), ((12, 2), "stage: lds")]:
+        ok = (s[:, i] > 0) & (s[:, j] > 0)
+        if ok.any():
+            d = s[ok, j] - s[ok, i]
+            print(f"    {name:20s} median {np.median(d):8.0f}  p90 {np.percentile(d,90):8.0f}")
     tot = s[:, 10] - s[:, 0]
     print(f"  {'whole wave':22s} median {np.median(tot):8.0f}  p90 {np.percentile(tot,90):8.0f}  max {tot.max():8d}")
 
