@@ -19,6 +19,10 @@
  *   - One handle per (device, stream); a handle is not thread-safe.
  *   - Coordinates are in the PADDED grid (the reference pads every map with a
  *     -1 border, dec_grid_rl.py:471-472): x in [0, width), y in [0, length).
+ *   - Bit maps (MC_FIELD_FREE/OBST/VISITED/GRID_*) are 8x8-cell tiles: uint64
+ *     [...][tile_rows][tile_cols], bit 8*r + c of tile (ti, tj) = cell
+ *     (8*ti + r, 8*tj + c).  Cells of edge tiles beyond the grid are set in
+ *     GRID_NEG (out of bounds = blocked) and clear in every other map.
  */
 #ifndef MARLCOV_H
 #define MARLCOV_H
@@ -30,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 1
+#define MARLCOV_ABI_VERSION 2
 
 enum {
   MC_OK = 0,
@@ -77,8 +81,8 @@ typedef struct mc_config {
   int32_t comm_radius;        /* 'comm_radius' (Chebyshev)                    */
   int32_t map_sharing;        /* 'map_sharing'                                */
   int32_t single_square_tool; /* 'single_square_tool'                         */
-  int32_t dist_reward;        /* 'dist_reward'   (must be 0 in ABI v1)        */
-  int32_t dijkstra_input;     /* 'dijkstra_input' (must be 0 in ABI v1)       */
+  int32_t dist_reward;        /* 'dist_reward'   (must be 0: not in the HIP path yet) */
+  int32_t dijkstra_input;     /* 'dijkstra_input' (must be 0: not in the HIP path yet) */
   int32_t auto_reset;         /* batch extra: re-place agents on done         */
   int32_t reset_grid_mode;    /* 0: keep the env's grid on reset;
                                  1: draw a grid uniformly from the pool       */
@@ -87,12 +91,14 @@ typedef struct mc_config {
 
 /* Derived geometry (mc_query). */
 typedef struct mc_layout {
-  int32_t words_per_row;      /* ceil(length / 64)                            */
-  int32_t window_half;        /* H: rows/cols staged per agent = 2H+1         */
+  int32_t tile_rows;          /* ceil(width / 8)                              */
+  int32_t tile_cols;          /* ceil(length / 8)                             */
+  int32_t window_half;        /* H = max(ceil(range), egoradius)              */
+  int32_t window_tiles;       /* TW: tiles per side staged per agent          */
   int32_t obs_layers;         /* Lc (3 + dist_reward + dijkstra_input)        */
   int32_t obs_side;           /* E = 2*egoradius + 1                          */
   int64_t obs_bytes_per_env;  /* N*Lc*E*E (uint8 obs)                         */
-  int64_t mask_words_per_agent; /* width * words_per_row                       */
+  int64_t mask_words_per_agent; /* tile_rows * tile_cols                      */
   int64_t state_bytes;        /* device bytes owned by the handle             */
 } mc_layout;
 
@@ -100,9 +106,9 @@ typedef struct mc_layout {
 enum {
   MC_FIELD_POS = 0,          /* int32 [B][N][2] (x, y)                         */
   MC_FIELD_MOVED = 1,        /* uint64 [B]  bit i: robot i is in robot_pad     */
-  MC_FIELD_FREE = 2,         /* uint64 [B][N][width][words_per_row] _free_pad  */
-  MC_FIELD_OBST = 3,         /* uint64 [B][N][width][words_per_row] _obst_pad  */
-  MC_FIELD_VISITED = 4,      /* uint64 [B][width][words_per_row]    _visited   */
+  MC_FIELD_FREE = 2,         /* uint64 [B][N][tile_rows][tile_cols] _free_pad  */
+  MC_FIELD_OBST = 3,         /* uint64 [B][N][tile_rows][tile_cols] _obst_pad  */
+  MC_FIELD_VISITED = 4,      /* uint64 [B][tile_rows][tile_cols]    _visited   */
   MC_FIELD_FREE_COUNT = 5,   /* uint32 [B]  count_nonzero(_free_pad > 0)       */
   MC_FIELD_VISITED_COUNT = 6,/* uint32 [B]  sum(_visited)                      */
   MC_FIELD_CURRSTEP = 7,     /* int32  [B]  _currstep                          */
@@ -110,8 +116,8 @@ enum {
   MC_FIELD_ENV_GRID = 9,     /* int32  [B]  grid pool index of each env        */
   MC_FIELD_EPISODE = 10,     /* uint32 [B]  resets so far (RNG counter)        */
   MC_FIELD_NUMFREE = 11,     /* int32  [G]  count_nonzero(grid > 0) per grid   */
-  MC_FIELD_GRID_NEG = 12,    /* uint64 [G][width][words_per_row] grid < 0      */
-  MC_FIELD_GRID_POS = 13,    /* uint64 [G][width][words_per_row] grid > 0      */
+  MC_FIELD_GRID_NEG = 12,    /* uint64 [G][tile_rows][tile_cols] grid < 0      */
+  MC_FIELD_GRID_POS = 13,    /* uint64 [G][tile_rows][tile_cols] grid > 0      */
   MC_FIELD_COUNT = 14
 };
 

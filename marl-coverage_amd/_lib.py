@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
@@ -58,8 +58,10 @@ class McLayout(ctypes.Structure):
     """Mirror of ``mc_layout``."""
 
     _fields_ = [
-        ("words_per_row", ctypes.c_int32),
+        ("tile_rows", ctypes.c_int32),
+        ("tile_cols", ctypes.c_int32),
         ("window_half", ctypes.c_int32),
+        ("window_tiles", ctypes.c_int32),
         ("obs_layers", ctypes.c_int32),
         ("obs_side", ctypes.c_int32),
         ("obs_bytes_per_env", ctypes.c_int64),

@@ -132,7 +132,7 @@ class BatchCoverageEnv:
         lay = _lib.McLayout()
         _lib.check(self.lib.mc_query(self._h, ctypes.byref(lay)), "mc_query")
         self.layout = lay
-        self.words_per_row = lay.words_per_row
+        self.tile_rows, self.tile_cols = lay.tile_rows, lay.tile_cols
         self.obs_shape = (self.num_agents, lay.obs_layers, lay.obs_side, lay.obs_side)
         self.num_actions = 4
 
@@ -234,7 +234,7 @@ class BatchCoverageEnv:
     # ------------------------------------------------------------------
     def field_shape(self, field):
         B, N, G = self.num_envs, self.num_agents, self.num_grids
-        mw = (self.width, self.words_per_row)
+        mw = (self.tile_rows, self.tile_cols)  # 8x8-cell tiles (tiles.py)
         return {
             _lib.FIELD_POS: (B, N, 2), _lib.FIELD_MOVED: (B,), _lib.FIELD_FREE: (B, N) + mw,
             _lib.FIELD_OBST: (B, N) + mw, _lib.FIELD_VISITED: (B,) + mw, _lib.FIELD_FREE_COUNT: (B,),

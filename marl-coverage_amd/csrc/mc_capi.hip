@@ -69,7 +69,7 @@ struct FieldDesc {
 
 FieldDesc field(Env* E, int f) {
   const mc::State& s = E->s;
-  const int64_t B = s.B, N = s.N, mw = (int64_t)s.Wp * s.nw, G = s.G;
+  const int64_t B = s.B, N = s.N, mw = (int64_t)s.TR * s.TC, G = s.G;
   switch (f) {
     case MC_FIELD_POS: return {s.pos, B * N * 2 * 4};
     case MC_FIELD_MOVED: return {s.moved, B * 8};
@@ -99,10 +99,10 @@ int dev_alloc(Env* E, void** p, size_t bytes) {
 }
 
 int env_threads(const mc::State& s) {
-  // every lane stages at most kMaxItemsPerLane (agent, row) items; beyond
+  // every lane stages at most kMaxItemsPerLane (agent, tile) items; beyond
   // that, prefer one wave per env (no cross-wave barriers) unless the beam
   // march would need more than ~8 sequential rounds per lane
-  const int items = s.N * s.We;
+  const int items = s.N * s.TW * s.TW;
   int nt = 64;
   while (nt < 1024 && items > mc::kMaxItemsPerLane * nt) nt *= 2;
   if (s.sensor == MC_SENSOR_LIDAR)
@@ -157,7 +157,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   if (c.egoradius < 0) return fail(MC_EINVAL, "egoradius must be >= 0");
   if (c.pad < c.egoradius) return fail(MC_EINVAL, "pad must be >= egoradius");
   if (c.dist_reward || c.dijkstra_input)
-    return fail(MC_EINVAL, "dist_reward / dijkstra_input layers are not in ABI v1");
+    return fail(MC_EINVAL, "dist_reward / dijkstra_input obs layers are not in the HIP path yet");
   if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
   if (c.maxsteps < 0) return fail(MC_EINVAL, "maxsteps must be >= 0");
 
@@ -172,11 +172,15 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     hs = c.square_radius;
   }
   const int H = hs > c.egoradius ? hs : c.egoradius;
-  if (2 * H + 3 > 63)
-    return fail(MC_EINVAL, "staged window 2H+3 = %d exceeds 63 (range/egoradius too large)", 2 * H + 3);
-  if ((int64_t)c.num_agents * (2 * H + 3) > 2 * 1024)
-    return fail(MC_EINVAL, "numrobot * (2H+3) = %d staged rows exceeds 2048",
-                c.num_agents * (2 * H + 3));
+  const int TW = mc::window_tiles(H);
+  if (2 * c.egoradius + 1 > 32)
+    return fail(MC_EINVAL, "egoradius %d > 15: obs crop rows are 32-bit", c.egoradius);
+  if ((int64_t)c.num_agents * TW * TW > (int64_t)mc::kMaxItemsPerLane * 1024)
+    return fail(MC_EINVAL, "numrobot * %d^2 window tiles = %d exceeds %d (range/egoradius too large)",
+                TW, c.num_agents * TW * TW, mc::kMaxItemsPerLane * 1024);
+  if (mc::env_lds_bytes(c.num_agents, TW, c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0, 3,
+                        2 * c.egoradius + 1) > 65536)
+    return fail(MC_EINVAL, "per-env LDS window exceeds 64 KiB (numrobot / range / num_lasers too large)");
 
   Env* E = new Env();
   E->cfg = c;
@@ -187,11 +191,13 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.N = c.num_agents;
   s.Wp = c.width;
   s.Lp = c.length;
-  s.nw = (c.length + 63) / 64;
+  s.TR = (c.width + 7) / 8;
+  s.TC = (c.length + 7) / 8;
   s.G = c.num_grids;
   s.H = H;
-  s.We = 2 * H + 3;
-  s.mg_We = mc::magic_div((uint32_t)s.We);
+  s.TW = TW;
+  s.mg_TW = mc::magic_div((uint32_t)TW);
+  s.mg_TW2 = mc::magic_div((uint32_t)(TW * TW));
   s.ego = c.egoradius;
   s.E = 2 * c.egoradius + 1;
   s.Lc = 3;
@@ -216,7 +222,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     delete E;
     return fail(MC_EHIP, "hipSetDevice(%d): %s", hip_device, hipGetErrorString(he));
   }
-  const size_t B = s.B, N = s.N, mw = (size_t)s.Wp * s.nw, G = s.G;
+  const size_t B = s.B, N = s.N, mw = (size_t)s.TR * s.TC, G = s.G;
   void* p = nullptr;
   int rc = MC_OK;
   size_t total = 0;
@@ -269,8 +275,10 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   }
   E->epw = mc::env_pack(s);
   mc_layout& L = E->lay;
-  L.words_per_row = s.nw;
+  L.tile_rows = s.TR;
+  L.tile_cols = s.TC;
   L.window_half = s.H;
+  L.window_tiles = s.TW;
   L.obs_layers = s.Lc;
   L.obs_side = s.E;
   L.obs_bytes_per_env = (int64_t)N * s.Lc * s.E * s.E;
@@ -513,7 +521,7 @@ int mc_check(void* env, void* stream) {
   if (err) {
     HIP_TRY(hipMemsetAsync(E->s.err, 0, 4, st));
     HIP_TRY(hipStreamSynchronize(st));
-    return fail(MC_EDEVICE, "device error word 0x%x (1=window 2=out-of-grid 4=placement 8=inject)", err);
+    return fail(MC_EDEVICE, "device error word 0x%x (1=window 4=placement 8=inject)", err);
   }
   return MC_OK;
 }

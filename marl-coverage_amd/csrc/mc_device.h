@@ -7,11 +7,6 @@
 
 namespace mc {
 
-// bits [off, off+64) of the 128-bit value hi:lo
-__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, int off) {
-  return off ? ((lo >> off) | (hi << (64 - off))) : lo;
-}
-
 __device__ __forceinline__ uint64_t low_mask(int w) {
   return w >= 64 ? ~0ull : ((1ull << w) - 1ull);
 }
@@ -35,11 +30,35 @@ __device__ __forceinline__ uint32_t bounded(uint32_t r, uint32_t n) {
   return (uint32_t)(((uint64_t)r * n) >> 32);
 }
 
+// bit of cell (r, c) inside its 8x8 tile
+__device__ __forceinline__ int tile_bit(int r, int c) { return ((r & 7) << 3) | (c & 7); }
+
 // isInBounds + grid < 0 (dec_grid_rl.py:284-295, :310) read from HBM
 __device__ __forceinline__ bool grid_blocked(const State& s, int g, int x, int y) {
   if (x < 0 || y < 0 || x >= s.Wp || y >= s.Lp) return true;
-  const uint64_t wv = s.grid_neg[((size_t)g * s.Wp + x) * s.nw + (y >> 6)];
-  return (wv >> (y & 63)) & 1ull;
+  const uint64_t t = s.grid_neg[((size_t)g * s.TR + (x >> 3)) * s.TC + (y >> 3)];
+  return (t >> tile_bit(x, y)) & 1ull;
+}
+
+// cells of global tile (ti, tj) that lie inside the padded grid
+__device__ __forceinline__ uint64_t tile_in_grid(const State& s, int ti, int tj) {
+  const int rv = s.Wp - 8 * ti, cv = s.Lp - 8 * tj;
+  if (rv >= 8 && cv >= 8) return ~0ull;
+  if (rv <= 0 || cv <= 0) return 0ull;
+  const uint64_t cols = (cv >= 8 ? 0xFFull : ((1ull << cv) - 1ull)) * 0x0101010101010101ull;
+  return cols & low_mask(8 * (rv >= 8 ? 8 : rv));
+}
+
+// rows [r0, r1] x cols [c0, c1] of a tile (inclusive, clamped to 0..7; empty
+// when r1 < r0 or c1 < c0)
+__device__ __forceinline__ uint64_t tile_rect(int r0, int r1, int c0, int c1) {
+  r0 = r0 < 0 ? 0 : r0;
+  c0 = c0 < 0 ? 0 : c0;
+  r1 = r1 > 7 ? 7 : r1;
+  c1 = c1 > 7 ? 7 : c1;
+  if (r1 < r0 || c1 < c0) return 0ull;
+  const uint64_t cols = (low_mask(c1 + 1) & ~low_mask(c0)) * 0x0101010101010101ull;
+  return cols & low_mask(8 * (r1 + 1)) & ~low_mask(8 * r0);
 }
 
 }  // namespace mc

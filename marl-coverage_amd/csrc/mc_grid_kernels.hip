@@ -15,14 +15,14 @@ namespace mc {
 // shareMaps (dec_grid_rl.py:423-447), run before the step kernel when
 // map_sharing is on: agent i's maps <- OR over {j: adj(i,j) or i==j}, with
 // adj from the positions at the start of the step (the last comm graph).
-// grid = (ceil(Wp*nw / 64), B); block = 64 lanes, one word position each.
+// grid = (ceil(TR*TC / 64), B); block = 64 lanes, one tile position each.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void share_kernel(State s, const uint8_t* __restrict__ actions) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int e = blockIdx.y;
   const int N = s.N;
   if (actions[(size_t)e * N] == 255) return;  // sentinel: no state change
-  const size_t mw = (size_t)s.Wp * s.nw;
+  const size_t mw = (size_t)s.TR * s.TC;
   const int lane = threadIdx.x;
   const size_t w = (size_t)blockIdx.x * 64 + lane;
   uint64_t* fo = reinterpret_cast<uint64_t*>(smem);   // [N][64]
@@ -63,23 +63,27 @@ __global__ __launch_bounds__(64) void share_kernel(State s, const uint8_t* __res
 // --------------------------------------------------------------------------
 // grid pool upload / generation
 // --------------------------------------------------------------------------
-// int8 [G][Wp][Lp] -> neg/pos bit planes, numfree[g] = count(grid > 0).
+// int8 [G][Wp][Lp] -> neg/pos tiles, numfree[g] = count(grid > 0).  Cells of
+// an edge tile beyond the grid are obstacles (isInBounds).
 __global__ void pack_grids_kernel(State s, const int8_t* __restrict__ grids) {
-  const size_t mw = (size_t)s.Wp * s.nw;
-  const size_t total = (size_t)s.G * mw;
+  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t total = (size_t)s.G * mt;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
-    const int g = (int)(i / mw);
-    const size_t rem = i - (size_t)g * mw;
-    const int x = (int)(rem / s.nw), w = (int)(rem - (size_t)x * s.nw);
-    const int8_t* row = grids + ((size_t)g * s.Wp + x) * s.Lp;
+    const int g = (int)(i / mt);
+    const size_t rem = i - (size_t)g * mt;
+    const int ti = (int)(rem / s.TC), tj = (int)(rem - (size_t)ti * s.TC);
     uint64_t neg = 0, pos = 0;
-    for (int b = 0; b < 64; ++b) {
-      const int y = w * 64 + b;
-      if (y >= s.Lp) { neg |= 1ull << b; continue; }
-      const int8_t v = row[y];
-      if (v < 0) neg |= 1ull << b;
-      if (v > 0) pos |= 1ull << b;
+    for (int r = 0; r < 8; ++r) {
+      const int x = 8 * ti + r;
+      for (int c = 0; c < 8; ++c) {
+        const int y = 8 * tj + c;
+        const uint64_t bit = 1ull << (8 * r + c);
+        if (x >= s.Wp || y >= s.Lp) { neg |= bit; continue; }
+        const int8_t v = grids[((size_t)g * s.Wp + x) * s.Lp + y];
+        if (v < 0) neg |= bit;
+        if (v > 0) pos |= bit;
+      }
     }
     const_cast<uint64_t*>(s.grid_neg)[i] = neg;
     const_cast<uint64_t*>(s.grid_pos)[i] = pos;
@@ -88,28 +92,32 @@ __global__ void pack_grids_kernel(State s, const int8_t* __restrict__ grids) {
 }
 
 // Bernoulli(p) obstacles in the interior, -1 border (gridgen semantics,
-// Utils/gridmaker.py:127-128, plus the np.pad of dec_grid_rl.py:471).
+// Utils/gridmaker.py:127-128, plus the np.pad of dec_grid_rl.py:471).  One
+// Philox block per tile row: 8 cells x 32 bits = 2 calls.
 __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int all_free) {
-  const size_t mw = (size_t)s.Wp * s.nw;
-  const size_t total = (size_t)s.G * mw;
+  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t total = (size_t)s.G * mt;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
-    const int g = (int)(i / mw);
-    const size_t rem = i - (size_t)g * mw;
-    const int x = (int)(rem / s.nw), w = (int)(rem - (size_t)x * s.nw);
+    const int g = (int)(i / mt);
+    const size_t rem = i - (size_t)g * mt;
+    const int ti = (int)(rem / s.TC), tj = (int)(rem - (size_t)ti * s.TC);
     uint64_t neg = 0;
-    for (int q = 0; q < 16; ++q) {
-      const uint4 r = philox(seed, make_uint4((uint32_t)g, (uint32_t)x, (uint32_t)(w * 16 + q), 0x67656e21u));
-      const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
-      for (int t = 0; t < 4; ++t) {
-        const int b = q * 4 + t;
-        const int y = w * 64 + b;
-        const bool border = x == 0 || x == s.Wp - 1 || y == 0 || y >= s.Lp - 1;
-        if (border || (!all_free && rv[t] < thresh)) neg |= 1ull << b;
+    for (int r = 0; r < 8; ++r) {
+      const int x = 8 * ti + r;
+      for (int h = 0; h < 2; ++h) {
+        const uint4 q = philox(seed, make_uint4((uint32_t)g, (uint32_t)x, (uint32_t)(tj * 2 + h), 0x67656e21u));
+        const uint32_t rv[4] = {q.x, q.y, q.z, q.w};
+        for (int t = 0; t < 4; ++t) {
+          const int c = h * 4 + t;
+          const int y = 8 * tj + c;
+          const bool outside = x >= s.Wp || y >= s.Lp;
+          const bool border = x == 0 || x == s.Wp - 1 || y == 0 || y == s.Lp - 1;
+          if (outside || border || (!all_free && rv[t] < thresh)) neg |= 1ull << (8 * r + c);
+        }
       }
     }
-    const uint64_t valid = (w == s.nw - 1 && (s.Lp & 63)) ? low_mask(s.Lp & 63) : ~0ull;
-    const uint64_t pos = ~neg & valid;
+    const uint64_t pos = ~neg;  // outside cells are in neg
     const_cast<uint64_t*>(s.grid_neg)[i] = neg;
     const_cast<uint64_t*>(s.grid_pos)[i] = pos;
     if (pos) atomicAdd(const_cast<int32_t*>(&s.numfree[g]), (int32_t)__popcll(pos));
@@ -117,7 +125,7 @@ __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int al
 }
 
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream) {
-  const size_t mw = (size_t)s.Wp * s.nw;
+  const size_t mw = (size_t)s.TR * s.TC;
   dim3 grid((unsigned)((mw + 63) / 64), s.B), block(64);
   const size_t lds = (size_t)s.N * 64 * 16 + 64 * 8;
   hipLaunchKernelGGL(share_kernel, grid, block, lds, stream, s, actions);
@@ -125,14 +133,14 @@ hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stre
 }
 
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream) {
-  const size_t total = (size_t)s.G * s.Wp * s.nw;
+  const size_t total = (size_t)s.G * s.TR * s.TC;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   hipLaunchKernelGGL(pack_grids_kernel, dim3(blocks), dim3(256), 0, stream, s, grids);
   return hipGetLastError();
 }
 
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream) {
-  const size_t total = (size_t)s.G * s.Wp * s.nw;
+  const size_t total = (size_t)s.G * s.TR * s.TC;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   double t = p * 4294967296.0;
   uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (t <= 0.0 ? 0u : (uint32_t)t);

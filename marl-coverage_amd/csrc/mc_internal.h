@@ -35,18 +35,24 @@ struct Beam {
 };
 static_assert(sizeof(Beam) == 16, "Beam is 16 bytes");
 
+
+// Bit maps are stored as 8x8 cell tiles: one u64 per tile, bit 8*r + c =
+// cell (8*ti + r, 8*tj + c).  A tile row is contiguous, so an agent's window
+// (a TW x TW block of tiles) is TW coalesced runs of TW words.  Cells of an
+// edge tile beyond the padded grid are obstacles in grid_neg and never set in
+// the other maps.
+//
 // Everything a kernel needs, passed by value.  Layout (all device memory):
-//   grid_neg/grid_pos  u64 [G][Wp][nw]     bit y%64 of word y/64 = cell (x,y)
-//   freem/obstm        u64 [B][N][Wp][nw]  per-agent _free_pad/_obst_pad
-//                                          (padded-grid region only: the
-//                                          reference never marks the pad ring)
-//   vis                u64 [B][Wp][nw]     _visited (union of free maps)
+//   grid_neg/grid_pos  u64 [G][TR][TC]     tiles of grid < 0 / grid > 0
+//   freem/obstm        u64 [B][N][TR][TC]  per-agent _free_pad/_obst_pad
+//   vis                u64 [B][TR][TC]     _visited (union of free maps)
 //   pos                i32 [B][N][2]       (_xinds, _yinds)
 struct State {
-  int B, N, Wp, Lp, nw, G;
+  int B, N, Wp, Lp, G;
+  int TR, TC;              // tile rows / columns of a map: ceil(Wp/8), ceil(Lp/8)
   int H;                   // sensing half-width (>= egoradius)
-  int We;                  // staged rows/cols per agent: 2H+3 (window +-1 for the move)
-  uint32_t mg_We, mg_LcE, mg_E, mg_nb;  // magic reciprocals: n / d == umulhi(n, mg_d)
+  int TW;                  // window tiles per side (window_tiles(H))
+  uint32_t mg_TW2, mg_TW, mg_LcE, mg_E, mg_nb;  // magic reciprocals: n / d == umulhi(n, mg_d)
   int ego, E, Lc;          // egoradius, obs side, obs layers
   int sensor, nbeams, sq_r;
   double pen, term, dincr;
@@ -75,12 +81,30 @@ struct State {
   uint64_t* stamps;        // diagnostic builds (-DMC_STAMPS) only: [B][16] s_memtime
 };
 
-constexpr int kMaxItemsPerLane = 2;  // staged (agent, row) items per lane
+constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
+
+// Window tiles per side for half-width H.  The staged "extended window" of an
+// agent is the cells [x0-H-1, x0+H+1] around its pre-move cell (the +1 margin
+// covers every post-move window); its tile block starts at tile
+// floor((x0-H-1)/8), so 8*TW >= 7 + (2H+3).
+__host__ __device__ constexpr int window_tiles(int H) { return (2 * H + 3 + 7 + 7) / 8; }
 
 // floor(n / d) == umulhi(n, magic(d)) for 2 <= d < 2^16 and n * d < 2^32;
 // d == 1 (2^32 does not fit) is encoded as 0 and handled by the caller
 __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
   return d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d);
+}
+
+// LDS bytes of one env slot of the env kernel (host + device use the same carve).
+__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int Lc, int E) {
+  size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
+  b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
+  b += (((size_t)N * 6 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by
+  b += 64;                                             // scalars
+  b += ((size_t)N + 15) & ~(size_t)15;                 // actions
+  b += (((size_t)N * Lc * E * 4) + 15) & ~(size_t)15;  // obs rows (E-bit words)
+  b += 64 * 4;                                         // per-lane sink words (lidar marks)
+  return b;
 }
 
 // Compile-time shape of an env kernel instantiation: fields > 0 are baked in
@@ -90,30 +114,12 @@ __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
 template <int N_, int H_, int NB_, int EGO_, int KM_>
 struct Shape {
   static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_;
-  __host__ __device__ static bool matches(const struct State& s);
+  __host__ __device__ static bool matches(const State& s) {
+    return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
+           (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) && (EGO_ == 0 || s.ego == EGO_) &&
+           (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_));
+  }
 };
-
-// LDS bytes of the env kernel (host + device use the same carve).
-__host__ __device__ inline size_t env_lds_bytes(int N, int We, int nbeams, int Lc, int E,
-                                                size_t wbytes) {
-  const size_t items = (size_t)N * We;
-  size_t b = (6 * items * wbytes + 15) & ~(size_t)15;  // neg, pos, fold, oold, fp, op
-  b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;  // beams
-  b += (size_t)N * 16;                       // x0, y0, x, y
-  b += 64;                                   // scalars
-  b += ((size_t)N + 15) & ~(size_t)15;       // actions
-  b += (((size_t)N * Lc * E) + 15) & ~(size_t)15;  // obs rows (one E-bit byte each)
-  b = (b + 15) & ~(size_t)15;
-  b += 64 * wbytes;  // per-lane sink word for masked-off lidar marks
-  return b;
-}
-
-template <int N_, int H_, int NB_, int EGO_, int KM_>
-__host__ __device__ inline bool Shape<N_, H_, NB_, EGO_, KM_>::matches(const State& s) {
-  return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
-         (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) && (EGO_ == 0 || s.ego == EGO_) &&
-         (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_));
-}
 
 // overwrite the baked-in fields of a kernel's State copy with constants
 template <class SH>
@@ -121,8 +127,9 @@ __device__ __forceinline__ void specialize(State& s) {
   if constexpr (SH::N > 0) s.N = SH::N;
   if constexpr (SH::H > 0) {
     s.H = SH::H;
-    s.We = 2 * SH::H + 3;
-    s.mg_We = magic_div(2 * SH::H + 3);
+    s.TW = window_tiles(SH::H);
+    s.mg_TW = magic_div(window_tiles(SH::H));
+    s.mg_TW2 = magic_div(window_tiles(SH::H) * window_tiles(SH::H));
   }
   if constexpr (SH::NB > 0) {
     s.sensor = 0;

@@ -22,6 +22,7 @@ import numpy as np
 from . import _lib
 from .batch_env import BatchCoverageEnv, pad_grid
 from .sensors import make_sensor
+from .tiles import tiles_to_cells
 
 _DIRS = (0, 1, 2, 3)
 
@@ -240,12 +241,8 @@ class DecGridRL:
         return self._grid[x][y] < 0 or self._robot_pos_map[x][y] == 1
 
     # ---- reference state arrays, materialised from the device on demand ----
-    def _unpack(self, words):
-        W, L = self._gridwidth, self._gridlen
-        w = words.cpu().numpy().astype(np.uint64)
-        bits = np.unpackbits(w.view(np.uint8).reshape(w.shape[:-1] + (-1,)), axis=-1,
-                             bitorder="little")[..., :L]
-        return bits.reshape(w.shape[:-2] + (W, L)).astype(np.float64)
+    def _unpack(self, tiles):
+        return tiles_to_cells(tiles.cpu().numpy(), self._gridwidth, self._gridlen).astype(np.float64)
 
     def _padded(self, inner):
         p = self._pad

@@ -7,30 +7,29 @@ import numpy as np
 from oracle.cpu_ref import DecGridRLRef
 
 
-def unpack_words(words, length):
-    """int64 [..., nw] words -> uint8 [..., length] cells (bit y%64 of word y//64)."""
-    w = np.ascontiguousarray(np.asarray(words).astype(np.uint64))
-    b = np.unpackbits(w.view(np.uint8).reshape(w.shape[:-1] + (-1,)), axis=-1, bitorder="little")
-    return b[..., :length]
+def unpack_tiles(tiles, rows, cols):
+    """int64 [..., TR, TC] 8x8-cell tiles -> uint8 [..., rows, cols] cells."""
+    from marlcov.tiles import tiles_to_cells
+    return tiles_to_cells(tiles, rows, cols)
 
 
 def device_state(env):
     """Host copies of every per-env state field of a BatchCoverageEnv."""
     from marlcov import _lib
-    L = env.length
+    W, L = env.width, env.length
     st = {
         "pos": env.get_state(_lib.FIELD_POS).cpu().numpy(),
         "moved": env.get_state(_lib.FIELD_MOVED).cpu().numpy().astype(np.uint64),
-        "free": unpack_words(env.get_state(_lib.FIELD_FREE).cpu().numpy(), L),
-        "obst": unpack_words(env.get_state(_lib.FIELD_OBST).cpu().numpy(), L),
-        "vis": unpack_words(env.get_state(_lib.FIELD_VISITED).cpu().numpy(), L),
+        "free": unpack_tiles(env.get_state(_lib.FIELD_FREE).cpu().numpy(), W, L),
+        "obst": unpack_tiles(env.get_state(_lib.FIELD_OBST).cpu().numpy(), W, L),
+        "vis": unpack_tiles(env.get_state(_lib.FIELD_VISITED).cpu().numpy(), W, L),
         "free_cnt": env.get_state(_lib.FIELD_FREE_COUNT).cpu().numpy(),
         "vis_cnt": env.get_state(_lib.FIELD_VISITED_COUNT).cpu().numpy(),
         "currstep": env.get_state(_lib.FIELD_CURRSTEP).cpu().numpy(),
         "done_thresh": env.get_state(_lib.FIELD_DONE_THRESH).cpu().numpy(),
         "env_grid": env.get_state(_lib.FIELD_ENV_GRID).cpu().numpy(),
-        "neg": unpack_words(env.get_state(_lib.FIELD_GRID_NEG).cpu().numpy(), L),
-        "pos_plane": unpack_words(env.get_state(_lib.FIELD_GRID_POS).cpu().numpy(), L),
+        "neg": unpack_tiles(env.get_state(_lib.FIELD_GRID_NEG).cpu().numpy(), W, L),
+        "pos_plane": unpack_tiles(env.get_state(_lib.FIELD_GRID_POS).cpu().numpy(), W, L),
         "numfree": env.get_state(_lib.FIELD_NUMFREE).cpu().numpy(),
     }
     return st

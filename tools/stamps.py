@@ -16,9 +16,8 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "marl-coverage_amd")
 LIB = os.path.join(PKG, "libmarlcov_stamps.so")
 # MC_ABL timing ablations (wrong results): 1 lidar marks to the sink only,
-# 3 no sense, 4 merge without dedup, 5 no obs, 6 stage without the mask loads,
-# 7 stage loads at word-planar addresses
-ABLATIONS = (1, 3, 4, 5, 6, 7)
+# 3 no sense, 4 merge without dedup, 5 no obs, 6 stage without the mask loads
+ABLATIONS = (1, 3, 4, 5, 6)
 PHASES = ["rt1 pos/act/scalars", "rt2 stage", "moves", "sense", "merge", "reward",
           "store", "(reset)", "obs", "adj+drain"]
 
