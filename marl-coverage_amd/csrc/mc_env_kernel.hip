@@ -15,10 +15,12 @@
 //                 (visited) tiles — TW coalesced runs of TW words per plane.
 //                 The +1 margin covers every post-move window, so the moves,
 //                 the beam march and the merge need no further loads.
-//   LDS compute   moves (slot-serial in robot order), lidar or square sensing
-//                 as LDS bit tests + ds_or marks, merge with popcounts; agents'
-//                 blocks share the global tile grid, so the union dedup is a
-//                 tile-for-tile AND
+//   LDS compute   moves (slot-serial in robot order); lidar sensing as a beam
+//                 march over "row form" planes (one WT word per window row,
+//                 scattered from the tiles at stage time) with ds_or marks,
+//                 gathered back into tiles afterwards; square sensing directly
+//                 on tiles; merge with popcounts — agents' blocks share the
+//                 global tile grid, so the union dedup is a tile-for-tile AND
 //   stores        changed tiles (plain stores: one writer per agent tile),
 //                 newly covered union bits (global_atomic_or: agents' blocks
 //                 overlap), positions, counters, reward, done, obs
@@ -55,7 +57,6 @@ __device__ __forceinline__ int udiv(int n, uint32_t magic) {
 }
 
 __device__ __forceinline__ int rdlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
-__device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) { atomicOr((unsigned int*)p, v); }
 
 struct Scal {
   double pen;          // move penalties, accumulated in robot order
@@ -72,21 +73,26 @@ struct Scal {
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 
 // One env slot's LDS.  Tile planes are [N][TW][TW] u64 in the agent's block
-// coordinates; the march addresses them as u32 halves (rows 0-3 / 4-7).
+// coordinates.  Row planes are [N][8*TW+1] WT: row lx of agent a's block, bit ly
+// = cell (8*bx + lx, 8*by + ly); the lidar march and the moves read them.
+template <typename WT>
 struct Lds {
   uint64_t *neg, *pos, *fold, *oold, *fp, *op;
+  WT *negr, *fpr, *opr;
   Beam* beams;
   int32_t *x0, *y0, *x, *y;  // pre-move / post-move cells
   int32_t *bx, *by;          // tile-block origin (tile units) of each agent
   Scal* sc;
   uint8_t* act;
   uint32_t* obsrow;          // [N*Lc*E] E-bit crop rows
-  uint32_t* sink;            // [64] target of lidar marks a lane does not make
+  WT* sink;                  // [64] target of lidar marks a lane does not make
 };
 
-__device__ __forceinline__ Lds carve(char* smem, const State& s) {
-  Lds L;
+template <typename WT>
+__device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
+  Lds<WT> L;
   const int tiles = s.N * s.TW * s.TW;
+  const int rows = s.N * (8 * s.TW + 1);
   uint64_t* p = reinterpret_cast<uint64_t*>(smem);
   L.neg = p;
   L.pos = p + tiles;
@@ -95,6 +101,10 @@ __device__ __forceinline__ Lds carve(char* smem, const State& s) {
   L.fp = p + 4 * tiles;
   L.op = p + 5 * tiles;
   char* q = smem + (size_t)6 * tiles * 8;
+  L.negr = reinterpret_cast<WT*>(q);
+  L.fpr = L.negr + rows;
+  L.opr = L.fpr + rows;
+  q += (((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15;
   L.beams = reinterpret_cast<Beam*>(q);
   q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
   L.x0 = reinterpret_cast<int32_t*>(q);
@@ -110,12 +120,12 @@ __device__ __forceinline__ Lds carve(char* smem, const State& s) {
   q += ((size_t)s.N + 15) & ~(size_t)15;
   L.obsrow = reinterpret_cast<uint32_t*>(q);
   q += (((size_t)s.N * s.Lc * s.E * 4) + 15) & ~(size_t)15;
-  L.sink = reinterpret_cast<uint32_t*>(q);
+  L.sink = reinterpret_cast<WT*>(q);
   return L;
 }
 
 // one env slot of the workgroup
-template <int NT, int EPW>
+template <int NT, int EPW, typename WT>
 struct Ctx {
   static constexpr int LPE = NT / EPW;            // lanes per env
   static constexpr int KI = kMaxItemsPerLane;     // staged tiles per lane
@@ -123,22 +133,22 @@ struct Ctx {
   int sub;    // lane within the env
   int lane0;  // first lane of this env's slot within the wave
   int e;      // env index
-  Lds L;
+  Lds<WT> L;
 };
 
 // broadcast lane (lane0 + i)'s value of v to the slot
-template <int NT, int EPW>
-__device__ __forceinline__ int bcast(const Ctx<NT, EPW>& C, int v, int i) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ int bcast(const Ctx<NT, EPW, WT>& C, int v, int i) {
   if constexpr (EPW == 1) return rdlane(v, i);
   else return __shfl(v, C.lane0 + i);
 }
 
 // ballot restricted to this env's slot (bit j = lane lane0 + j)
-template <int NT, int EPW>
-__device__ __forceinline__ uint64_t slot_ballot(const Ctx<NT, EPW>& C, bool p) {
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ uint64_t slot_ballot(const Ctx<NT, EPW, WT>& C, bool p) {
   const uint64_t m = __ballot(p);
   if constexpr (EPW == 1) return m;
-  else return (m >> C.lane0) & low_mask(Ctx<NT, EPW>::LPE);
+  else return (m >> C.lane0) & low_mask(Ctx<NT, EPW, WT>::LPE);
 }
 
 // staged (agent, tile) items of this lane; old HBM tiles stay in registers
@@ -152,14 +162,20 @@ struct Items {
   uint64_t nf[KI], no[KI], nu[KI];  // newly set bits
 };
 
+template <typename WT>
+__device__ __forceinline__ void lds_or(WT* p, WT v) {
+  if constexpr (sizeof(WT) == 4) atomicOr((unsigned int*)p, (unsigned int)v);
+  else atomicOr((unsigned long long*)p, (unsigned long long)v);
+}
+
 // --------------------------------------------------------------------------
 // stage: one round trip for every staged tile (masks known zero after reset)
 // --------------------------------------------------------------------------
-template <int NT, int EPW, int KI>
-__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW>& C, bool load_masks,
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, bool load_masks,
                                       Items<KI>& I) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  const Lds& L = C.L;
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   const int items = s.N * TW2;
   const size_t mt = (size_t)s.TR * s.TC;
@@ -169,6 +185,7 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW>& C, boo
   const bool square = s.sensor == 1;
   uint64_t n[KI], p[KI];
   size_t gt[KI], fb[KI];
+  int ti[KI], tj[KI];
   // addresses first, then every load of the lane back to back with no
   // exec-mask branches (tiles outside the map read tile 0 and are replaced)
 #pragma unroll
@@ -177,9 +194,9 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW>& C, boo
     const bool it = idx < items;
     const int a = it ? udiv(idx, s.mg_TW2) : 0;
     const int rem = idx - a * TW2;
-    const int ti = udiv(rem, s.mg_TW);
-    const int tj = rem - ti * TW;
-    const int gi = L.bx[a] + ti, gj = L.by[a] + tj;
+    ti[k] = udiv(rem, s.mg_TW);
+    tj[k] = rem - ti[k] * TW;
+    const int gi = L.bx[a] + ti[k], gj = L.by[a] + tj[k];
     I.a[k] = a;
     I.gi[k] = gi;
     I.gj[k] = gj;
@@ -201,11 +218,18 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW>& C, boo
 #pragma unroll
     for (int k = 0; k < KI; ++k) p[k] = gp[gt[k]];
   }
+  if (!square) {  // lidar mark rows start empty
+    for (int r = C.sub; r < s.N * (8 * TW + 1); r += LPE) {
+      L.fpr[r] = 0;
+      L.opr[r] = 0;
+    }
+  }
 #ifdef MC_STAMPS
   STAMP(11);  // loads issued
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   STAMP(12);  // loads landed
 #endif
+  uint8_t* nb = reinterpret_cast<uint8_t*>(L.negr);
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const bool in = I.in[k];
@@ -215,19 +239,29 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW>& C, boo
     I.u[k] = m ? I.u[k] : 0;
     const int idx = C.sub + k * LPE;
     if (idx < items) {
-      L.neg[idx] = in ? n[k] : ~0ull;
-      L.pos[idx] = (square && in) ? p[k] : 0ull;
+      const uint64_t nt = in ? n[k] : ~0ull;
+      if (square) {
+        L.neg[idx] = nt;
+        L.pos[idx] = in ? p[k] : 0ull;
+      }
       L.fold[idx] = I.f[k];
       L.oold[idx] = I.o[k];
-      L.fp[idx] = 0;
-      L.op[idx] = 0;
+      // scatter the tile's 8 row bytes into the row plane (byte tj of rows
+      // 8*ti .. 8*ti+7 of the agent's block)
+      uint8_t* dst = nb + ((size_t)(I.a[k] * (8 * TW + 1) + 8 * ti[k]) * sizeof(WT) + tj[k]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dst[r * sizeof(WT)] = (uint8_t)(nt >> (8 * r));
     }
   }
 }
 
-// bit of window cell (lx, ly) of agent a: LDS tile index and bit
-__device__ __forceinline__ int win_tile(const State& s, int a, int lx, int ly) {
-  return (a * s.TW + (lx >> 3)) * s.TW + (ly >> 3);
+// tile (ti, tj) of agent a gathered from a row plane (the inverse scatter)
+template <typename WT>
+__device__ __forceinline__ uint64_t gather_tile(const WT* rows, int r0, int tj) {
+  uint64_t t = 0;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) t |= (uint64_t)((rows[r0 + r] >> (8 * tj)) & (WT)0xFF) << (8 * r);
+  return t;
 }
 
 // --------------------------------------------------------------------------
@@ -237,9 +271,9 @@ __device__ __forceinline__ int win_tile(const State& s, int a, int lx, int ly) {
 // higher-index robot that has not moved yet (:186,190-199,310).  The grid
 // test reads the staged window (1 outside the map = isInBounds).
 // --------------------------------------------------------------------------
-template <int NT, int EPW>
-__device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW>& C, double pen_unit) {
-  const Lds& L = C.L;
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C, double pen_unit) {
+  const Lds<WT>& L = C.L;
   const int N = s.N;
   const bool live = C.sub < N;
   int x = live ? L.x0[C.sub] : INT32_MIN / 2;
@@ -249,7 +283,7 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW>& C, dou
   int gblk = 1;
   if (live && act < 4) {
     const int lx = x + dx - 8 * L.bx[C.sub], ly = y + dy - 8 * L.by[C.sub];
-    gblk = (int)((L.neg[win_tile(s, C.sub, lx, ly)] >> tile_bit(lx, ly)) & 1ull);
+    gblk = (int)((L.negr[C.sub * (8 * s.TW + 1) + lx] >> ly) & (WT)1);
   }
   const int tx = x + dx, ty = y + dy;
   double pen = 0.0;
@@ -274,29 +308,28 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW>& C, dou
 // encodes the reference's float64 `+=` chain bit-exactly (mc_internal.h).
 // Every cell of a beam lies within Chebyshev K <= H of the post-move robot,
 // which is within 1 of the staged window's centre: no window check is needed
-// (mc_set_beam_table rejects K > H).  A ray's cell is addressed as a u32 half
-// tile (rows 0-3 / 4-7) of the agent's block.
+// (mc_set_beam_table rejects K > H).  Row planes: the cell's word is one add,
+// its bit one shift.
 // --------------------------------------------------------------------------
 struct Ray {
   uint32_t bits;     // minor-move bit per step (K <= 31)
-  int lx, ly;        // current cell in the agent's block coordinates
+  int row, col;      // current cell: row-plane index (agent base + lx), ly
   int drow, dcol;    // major step
   int mrow, mcol;    // minor step (when the step's bit is set)
-  int base;          // a * TW (tile-row base of the agent's block)
   int K;
   bool live;
 };
 
-__device__ __forceinline__ Ray ray_init(const State& s, const Lds& L, int idx) {
+template <typename WT>
+__device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int idx) {
   Ray R;
   R.live = idx < s.N * s.nbeams;
   const int a = R.live ? udiv(idx, s.mg_nb) : 0;
   const int b = R.live ? idx - a * s.nbeams : 0;
   const Beam bm = L.beams[b];
   const int xa = L.x[a], ya = L.y[a];
-  R.lx = xa - 8 * L.bx[a];
-  R.ly = ya - 8 * L.by[a];
-  R.base = a * s.TW;
+  R.row = a * (8 * s.TW + 1) + xa - 8 * L.bx[a];
+  R.col = ya - 8 * L.by[a];
   const bool ax = bm.axis == 0;
   R.drow = ax ? bm.sign : 0;
   R.dcol = ax ? 0 : bm.sign;
@@ -309,76 +342,80 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds& L, int idx) {
 
 __device__ __forceinline__ void ray_advance(Ray& R, int k) {
   const bool mv = (R.bits >> k) & 1u;
-  R.lx += R.drow + (mv ? R.mrow : 0);
-  R.ly += R.dcol + (mv ? R.mcol : 0);
-}
-
-// u32 word (half tile) of the ray's cell and its bit
-__device__ __forceinline__ int ray_word(const State& s, const Ray& R) {
-  return (((R.base + (R.lx >> 3)) * s.TW + (R.ly >> 3)) << 1) | ((R.lx >> 2) & 1);
-}
-__device__ __forceinline__ uint32_t ray_bit(const Ray& R) {
-  return 1u << (((R.lx & 3) << 3) | (R.ly & 7));
+  R.row += R.drow + (mv ? R.mrow : 0);
+  R.col += R.dcol + (mv ? R.mcol : 0);
 }
 
 // Branch-free mark: every lane issues one ds_or per ray and step; a lane with
 // nothing to mark ORs into its own sink word (no bank conflicts, no exec-mask
 // branches).  Re-marking an already free cell is harmless (OR).
-__device__ __forceinline__ void ray_mark(const Lds& L, Ray& R, int k, int w, uint32_t bit,
-                                         uint32_t nrow, uint32_t* sink) {
+template <typename WT>
+__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT* sink) {
   const bool on = R.live && k <= R.K;
+  const WT bit = (WT)1 << R.col;
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
-  uint32_t* fp32 = reinterpret_cast<uint32_t*>(L.fp);
-  uint32_t* op32 = reinterpret_cast<uint32_t*>(L.op);
 #if defined(MC_ABL) && MC_ABL == 1
-  lds_or(sink, bit);  // timing ablation: no marks
+  lds_or<WT>(sink, bit);  // timing ablation: no marks
 #else
-  lds_or(on ? (hit ? op32 : fp32) + w : sink, bit);
+  lds_or<WT>(on ? (hit ? L.opr : L.fpr) + R.row : sink, bit);
 #endif
   R.live = on && !hit;
 }
 
-template <int NT, int EPW>
-__device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW>& C) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  constexpr int RPL = Ctx<NT, EPW>::RPL;
-  const Lds& L = C.L;
+template <int NT, int EPW, typename WT, int SUK>
+__device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int RPL = Ctx<NT, EPW, WT>::RPL;
+  constexpr int SU = SUK;
+  const Lds<WT>& L = C.L;
   const int N = s.N, TW = s.TW, TW2 = TW * TW;
   if (s.sensor == 0) {
     // step 0 of every beam is the robot's own (free) cell: mark it once
-    for (int a = C.sub; a < N; a += LPE) {
-      const int lx = L.x[a] - 8 * L.bx[a], ly = L.y[a] - 8 * L.by[a];
-      atomicOr((unsigned long long*)&L.fp[win_tile(s, a, lx, ly)], 1ull << tile_bit(lx, ly));
-    }
-    const uint32_t* neg32 = reinterpret_cast<const uint32_t*>(L.neg);
-    uint32_t* sink = L.sink + (threadIdx.x & 63);
+    for (int a = C.sub; a < N; a += LPE)
+      lds_or<WT>(&L.fpr[a * (8 * TW + 1) + L.x[a] - 8 * L.bx[a]], (WT)1 << (L.y[a] - 8 * L.by[a]));
+    WT* sink = L.sink + (threadIdx.x & 63);
     const int total = N * s.nbeams;
     // lane l of a pass takes rays RPL*l .. RPL*l+RPL-1: within one ds_or the
     // lanes of an agent hold beams RPL apart, which mostly land in different
-    // words (fewer same-address LDS atomics than adjacent beams)
+    // rows (fewer same-address LDS atomics than adjacent beams)
     for (int base = C.sub * RPL; base < total; base += RPL * LPE) {
       Ray q[RPL];
 #pragma unroll
       for (int j = 0; j < RPL; ++j) {
-        q[j] = ray_init(s, L, base + j);
+        q[j] = ray_init<WT>(s, L, base + j);
         ray_advance(q[j], 0);
       }
       // wave-uniform trip count (every cell with k <= K <= beam_kmax <= H
-      // lies inside the staged window)
+      // lies inside the staged window).  SU steps per batch: the batch's row
+      // reads are all issued before its first mark, so no read waits behind
+      // an LDS atomic (LDS ops complete in order).
       const int kmax = s.beam_kmax;
-      for (int k = 1; k <= kmax; ++k) {
-        int w[RPL];
-        uint32_t bit[RPL], nr[RPL];
+      for (int k0 = 1; k0 <= kmax; k0 += SU) {
+        WT nr[SU][RPL];
+        Ray q0[RPL];
 #pragma unroll
-        for (int j = 0; j < RPL; ++j) {  // all word reads of this step in flight
-          w[j] = ray_word(s, q[j]);
-          bit[j] = ray_bit(q[j]);
-          nr[j] = neg32[w[j]];
+        for (int j = 0; j < RPL; ++j) q0[j] = q[j];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          if (k0 + u <= kmax) {  // uniform
+#pragma unroll
+            for (int j = 0; j < RPL; ++j) {
+              nr[u][j] = L.negr[q[j].row];
+              ray_advance(q[j], k0 + u);
+            }
+          }
         }
 #pragma unroll
-        for (int j = 0; j < RPL; ++j) {
-          ray_mark(L, q[j], k, w[j], bit[j], nr[j], sink);
-          ray_advance(q[j], k);
+        for (int j = 0; j < RPL; ++j) q[j] = q0[j];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          if (k0 + u <= kmax) {
+#pragma unroll
+            for (int j = 0; j < RPL; ++j) {
+              ray_mark<WT>(L, q[j], k0 + u, nr[u][j], sink);
+              ray_advance(q[j], k0 + u);
+            }
+          }
         }
       }
     }
@@ -401,16 +438,38 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW>& C) {
   }
 }
 
+// lidar: mark rows -> mark tiles (after the march, before the merge)
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int KI = Ctx<NT, EPW, WT>::KI;
+  const Lds<WT>& L = C.L;
+  const int TW = s.TW, TW2 = TW * TW;
+  const int items = s.N * TW2;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = C.sub + k * LPE;
+    if (idx < items) {
+      const int a = udiv(idx, s.mg_TW2), rem = idx - a * TW2;
+      const int ti = udiv(rem, s.mg_TW), tj = rem - ti * TW;
+      const int r0 = a * (8 * TW + 1) + 8 * ti;
+      L.fp[idx] = gather_tile<WT>(L.fpr, r0, tj);
+      L.op[idx] = gather_tile<WT>(L.opr, r0, tj);
+    }
+  }
+}
+
 // single_square_tool: only the robot's own cell becomes free (:233-234)
-template <int NT, int EPW>
-__device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW>& C) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  const Lds& L = C.L;
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   for (int idx = C.sub; idx < s.N * TW2; idx += LPE) {
     const int a = udiv(idx, s.mg_TW2);
     const int lx = L.x[a] - 8 * L.bx[a], ly = L.y[a] - 8 * L.by[a];
-    L.fp[idx] = (win_tile(s, a, lx, ly) == idx) ? (1ull << tile_bit(lx, ly)) : 0ull;
+    const int own = (a * TW + (lx >> 3)) * TW + (ly >> 3);
+    L.fp[idx] = (own == idx) ? (1ull << tile_bit(lx, ly)) : 0ull;
   }
 }
 
@@ -422,10 +481,10 @@ __device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW>& 
 // every block that holds it.  Also folds the marks into the old tiles (the
 // obs crops read the post-step maps).
 // --------------------------------------------------------------------------
-template <int NT, int EPW, int KI>
-__device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW>& C, Items<KI>& I) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  const Lds& L = C.L;
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
   const int TW = s.TW;
   const int items = s.N * TW * TW;
   // EPW == 1: agent j's block origin in lane j of every wave, broadcast by
@@ -472,8 +531,9 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW>& C, Ite
   if (cv) atomicAdd(&L.sc->cnt_vis, cv);
 }
 
-template <int NT, int EPW, int KI>
-__device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW>& C, const Items<KI>& I) {
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, WT>& C,
+                                            const Items<KI>& I) {
   const size_t mt = (size_t)s.TR * s.TC;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
@@ -489,24 +549,47 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW>& 
   }
 }
 
+// sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
+template <int NT, int EPW, typename WT, int KI, int SUK>
+__device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
+                                                Items<KI>& I) {
+#if !(defined(MC_ABL) && MC_ABL == 3)
+  sense<NT, EPW, WT, SUK>(s, C);
+#endif
+  __syncthreads();
+  STAMP(13);
+  if (s.sensor == 0) {
+    gather_marks<NT, EPW, WT>(s, C);
+    __syncthreads();
+  }
+  STAMP(4);
+  if (s.sst) {
+    single_tool<NT, EPW, WT>(s, C);
+    __syncthreads();
+  }
+  merge<NT, EPW, WT, KI>(s, C, I);
+}
+
 // --------------------------------------------------------------------------
 // reset (dec_grid_rl.py:449-531) of the slot's env inside the launch: grid
 // pick, start cells (injected, or Philox rejection draw with the reference's
 // acceptance rule, :491-502), zeroed maps, initial observe() (reward
 // discarded, :524).
 // --------------------------------------------------------------------------
-template <int NT, int EPW>
-__device__ __forceinline__ void set_block(const State& s, const Lds& L, int a) {
-  L.bx[a] = (L.x0[a] - s.H - 1) >> 3;  // arithmetic shift: floor for negatives
-  L.by[a] = (L.y0[a] - s.H - 1) >> 3;
+template <typename WT>
+__device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int a, int x, int y) {
+  L.x0[a] = L.x[a] = x;
+  L.y0[a] = L.y[a] = y;
+  L.bx[a] = (x - s.H - 1) >> 3;  // arithmetic shift: floor for negatives
+  L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW>
-__device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW>& C,
+template <int NT, int EPW, typename WT, int SUK>
+__device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  constexpr int KI = Ctx<NT, EPW>::KI;
-  const Lds& L = C.L;
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int KI = Ctx<NT, EPW, WT>::KI;
+  const Lds<WT>& L = C.L;
   const int N = s.N;
   const int e = C.e;
   if (C.sub == 0) {
@@ -542,9 +625,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW>& C,
       for (int j = 0; j < C.sub; ++j)
         bad |= (inj_pos[((size_t)e * N + j) * 2] == x && inj_pos[((size_t)e * N + j) * 2 + 1] == y);
       if (bad) atomicOr(s.err, ERR_INJECT);
-      L.x0[C.sub] = L.x[C.sub] = x;
-      L.y0[C.sub] = L.y[C.sub] = y;
-      set_block<NT, EPW>(s, L, C.sub);
+      set_agent<WT>(s, L, C.sub, x, y);
     }
   } else if (C.sub < 64) {
     // x = randint(W), y = randint(L); accept iff grid >= 0 and unoccupied;
@@ -571,23 +652,16 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW>& C,
       }
     }
     if (placed < N && lane == 0) atomicOr(s.err, ERR_PLACEMENT);
-    if (lane < N) {
-      L.x0[lane] = L.x[lane] = px;
-      L.y0[lane] = L.y[lane] = py;
-      set_block<NT, EPW>(s, L, lane);
-    }
+    if (lane < N) set_agent<WT>(s, L, lane, px, py);
   }
   // the zeroing stores must land before the window stores / atomics below
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   Items<KI> I;
-  stage<NT, EPW, KI>(s, C, /*load_masks=*/false, I);
+  stage<NT, EPW, WT, KI>(s, C, /*load_masks=*/false, I);
   __syncthreads();
-  sense<NT, EPW>(s, C);
-  __syncthreads();
-  if (s.sst) { single_tool<NT, EPW>(s, C); __syncthreads(); }
-  merge<NT, EPW, KI>(s, C, I);
-  store_tiles<NT, EPW, KI>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
+  store_tiles<NT, EPW, WT, KI>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
     s.free_cnt[e] = L.sc->cnt_free;
@@ -601,11 +675,12 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW>& C,
 // E x E around each robot.  Each (agent, layer, row) becomes one E-bit word
 // in LDS; the uint8 output is then written as dwords.
 // --------------------------------------------------------------------------
-template <int NT, int EPW>
-__device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW>& C, uint8_t* obs_out) {
-  constexpr int LPE = Ctx<NT, EPW>::LPE;
-  const Lds& L = C.L;
-  const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc;
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>& C,
+                                          uint8_t* obs_out) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc, TW = s.TW;
   const uint64_t moved = L.sc->moved;
   const uint64_t emask = low_mask(E);
   for (int idx = C.sub; idx < N * Lc * E; idx += LPE) {
@@ -621,12 +696,12 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW>& C,
         if (L.x[j] == cx && dc >= 0 && dc < E) bits |= 1ull << dc;
       }
     } else if (layer <= 2) {
-      // crop row = bits [ly0, ly0+E) of window row lx, gathered from the
+      // crop row = bits [ly0, ly0+E) of block row lx, gathered from the
       // row's byte in consecutive tiles of the block
       const int lx = xa - ego + r - 8 * L.bx[a];
       const int ly0 = ya - ego - 8 * L.by[a];
       const uint64_t* plane = layer == 1 ? L.fold : L.oold;
-      const int t0 = win_tile(s, a, lx, ly0);
+      const int t0 = (a * TW + (lx >> 3)) * TW + (ly0 >> 3);
       const int sh = (lx & 7) * 8;
       const int nt = ((ly0 & 7) + E + 7) >> 3;
       uint64_t acc = 0;
@@ -661,7 +736,7 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW>& C,
 // --------------------------------------------------------------------------
 // the env kernel: EPW envs per workgroup
 // --------------------------------------------------------------------------
-template <int NT, int EPW, class SH>
+template <int NT, int EPW, typename WT, class SH>
 __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ env_mask,
                                                  const int32_t* __restrict__ inj_pos,
@@ -671,9 +746,11 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
                                                  uint8_t* __restrict__ adj_out) {
   State s = s_in;
   specialize<SH>(s);
-  using CtxT = Ctx<NT, EPW>;
+  using CtxT = Ctx<NT, EPW, WT>;
   constexpr int LPE = CtxT::LPE;
   constexpr int KI = CtxT::KI;
+  // march steps per batch: the whole march when the shape fixes beam_kmax
+  constexpr int SUK = SH::KM > 0 ? SH::KM : 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -684,9 +761,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   const int e_raw = blockIdx.x * EPW + slot;
   const bool valid = e_raw < s.B;  // a short last workgroup leaves a slot idle
   C.e = valid ? e_raw : s.B - 1;
-  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E);
-  C.L = carve(smem + slot * slot_lds, s);
-  const Lds& L = C.L;
+  const size_t slot_lds =
+      env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E, (int)sizeof(WT));
+  C.L = carve<WT>(smem + slot * slot_stride(slot_lds), s);
+  const Lds<WT>& L = C.L;
   const int e = C.e;
 
   const bool is_step = mode == MODE_STEP;
@@ -698,10 +776,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // ---- round trip 1: positions, actions, scalars, beam table ---------------
   if (C.sub < N) {
     const int2 p = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + C.sub];
-    L.x0[C.sub] = L.x[C.sub] = p.x;
-    L.y0[C.sub] = L.y[C.sub] = p.y;
-    L.bx[C.sub] = (p.x - s.H - 1) >> 3;
-    L.by[C.sub] = (p.y - s.H - 1) >> 3;
+    set_agent<WT>(s, L, C.sub, p.x, p.y);
     if (active) L.act[C.sub] = actions[(size_t)e * N + C.sub];
   }
   if (C.sub == 0) {
@@ -727,23 +802,17 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     STAMP(1);
     Items<KI> I;
 #if defined(MC_ABL) && MC_ABL == 6
-    stage<NT, EPW, KI>(s, C, false, I);  // timing ablation: grid tiles only
+    stage<NT, EPW, WT, KI>(s, C, false, I);  // timing ablation: grid tiles only
 #else
-    stage<NT, EPW, KI>(s, C, true, I);  // ---- round trip 2 ----
+    stage<NT, EPW, WT, KI>(s, C, true, I);  // ---- round trip 2 ----
 #endif
     if (C.sub == 0) L.sc->numfree = s.numfree[L.sc->grid];
     __syncthreads();
     STAMP(2);
-    if (C.sub < 64) moves<NT, EPW>(s, C, -s.pen);
+    if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
     __syncthreads();
     STAMP(3);
-#if !(defined(MC_ABL) && MC_ABL == 3)
-    sense<NT, EPW>(s, C);
-#endif
-    __syncthreads();
-    STAMP(4);
-    if (s.sst) { single_tool<NT, EPW>(s, C); __syncthreads(); }
-    merge<NT, EPW, KI>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
     __syncthreads();
     STAMP(5);
     if (C.sub == 0) {
@@ -772,18 +841,18 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     __syncthreads();
     STAMP(6);
     if (!L.sc->do_reset) {
-      store_tiles<NT, EPW, KI>(s, C, I);
+      store_tiles<NT, EPW, WT, KI>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req) {
-    reset_env<NT, EPW>(s, C, inj_pos);
+    reset_env<NT, EPW, WT, SUK>(s, C, inj_pos);
   } else {
     // sentinel step / env left out of a partial reset: obs of the current
     // state only (dec_grid_rl.py:104-107,160)
     Items<KI> I;
-    stage<NT, EPW, KI>(s, C, true, I);
+    stage<NT, EPW, WT, KI>(s, C, true, I);
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
@@ -798,7 +867,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   }
   STAMP(8);
 #if !(defined(MC_ABL) && MC_ABL == 5)
-  if (valid) write_obs<NT, EPW>(s, C, obs_out);
+  if (valid) write_obs<NT, EPW, WT>(s, C, obs_out);
 #endif
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
@@ -835,23 +904,36 @@ static bool getenv_spec() {
 hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
                       uint8_t* adj, int nt, int epw, hipStream_t stream) {
-  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E);
-#define MC_LAUNCH_SH(T, P, SH)                                                                  \
-  hipLaunchKernelGGL((env_kernel<T, P, SH>), dim3((s.B + (P)-1) / (P)), dim3(T), slot_lds * (P), \
-                     stream, s, mode, actions, env_mask, inj_pos, reward, done, obs, adj)
-#define MC_LAUNCH(T, P) MC_LAUNCH_SH(T, P, Dynamic)
+  const bool narrow = s.TW <= 4;  // window rows fit a u32
+  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
+                                        narrow ? 4 : 8);
+#define MC_LAUNCH_SH(T, P, W, SH)                                                              \
+  hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + (P)-1) / (P)), dim3(T),             \
+                     slot_stride(slot_lds) * (P), stream, s, mode, actions, env_mask, inj_pos,    \
+                     reward, done,                                                               \
+                     obs, adj)
+#define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
   using Dynamic = Shape<0, 0, 0, 0, 0>;
   using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
   if (epw == 2) {
-    if (getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, ShapeC2);
-    else MC_LAUNCH(64, 2);
+    if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
+    else if (narrow) MC_LAUNCH(64, 2, uint32_t);
+    else MC_LAUNCH(64, 2, uint64_t);
+  } else if (narrow) {
+    switch (nt) {
+      case 64: MC_LAUNCH(64, 1, uint32_t); break;
+      case 128: MC_LAUNCH(128, 1, uint32_t); break;
+      case 256: MC_LAUNCH(256, 1, uint32_t); break;
+      case 512: MC_LAUNCH(512, 1, uint32_t); break;
+      default: MC_LAUNCH(1024, 1, uint32_t); break;
+    }
   } else {
     switch (nt) {
-      case 64: MC_LAUNCH(64, 1); break;
-      case 128: MC_LAUNCH(128, 1); break;
-      case 256: MC_LAUNCH(256, 1); break;
-      case 512: MC_LAUNCH(512, 1); break;
-      default: MC_LAUNCH(1024, 1); break;
+      case 64: MC_LAUNCH(64, 1, uint64_t); break;
+      case 128: MC_LAUNCH(128, 1, uint64_t); break;
+      case 256: MC_LAUNCH(256, 1, uint64_t); break;
+      case 512: MC_LAUNCH(512, 1, uint64_t); break;
+      default: MC_LAUNCH(1024, 1, uint64_t); break;
     }
   }
 #undef MC_LAUNCH

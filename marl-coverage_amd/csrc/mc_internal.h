@@ -83,6 +83,12 @@ struct State {
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 
+// Lidar marks are made in "row form" (one u32/u64 per window row: the march's
+// address and bit are then one add and one shift), so a window row must fit
+// 64 bits: TW <= 8, i.e. H <= 27.  An agent's rows are 8*TW + 1 apart (odd:
+// the same row of different agents falls on different LDS banks).
+constexpr int kMaxWindowTiles = 8;
+
 // Window tiles per side for half-width H.  The staged "extended window" of an
 // agent is the cells [x0-H-1, x0+H+1] around its pre-move cell (the +1 margin
 // covers every post-move window); its tile block starts at tile
@@ -96,15 +102,24 @@ __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
 }
 
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
-__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int Lc, int E) {
+// rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
+__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int Lc, int E,
+                                                int rowbytes) {
   size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
+  b += (((size_t)3 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / fp / op rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
   b += (((size_t)N * 6 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by
   b += 64;                                             // scalars
   b += ((size_t)N + 15) & ~(size_t)15;                 // actions
   b += (((size_t)N * Lc * E * 4) + 15) & ~(size_t)15;  // obs rows (E-bit words)
-  b += 64 * 4;                                         // per-lane sink words (lidar marks)
+  b += 64 * (size_t)rowbytes;                          // per-lane sink words (lidar marks)
   return b;
+}
+
+// Byte stride between the env slots of a workgroup: skewed by 20 LDS banks so
+// the two slots' row planes do not fall on the same banks.
+__host__ __device__ inline size_t slot_stride(size_t slot_lds) {
+  return ((slot_lds + 255) & ~(size_t)255) + 80;
 }
 
 // Compile-time shape of an env kernel instantiation: fields > 0 are baked in
