@@ -180,8 +180,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
                 TW, c.num_agents * TW * TW, mc::kMaxItemsPerLane * 1024);
   if (TW > mc::kMaxWindowTiles)
     return fail(MC_EINVAL, "window half-width H = %d > 27 (range/egoradius too large)", H);
-  if (mc::env_lds_bytes(c.num_agents, TW, c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0, 3,
-                        2 * c.egoradius + 1, TW <= 4 ? 4 : 8) > 65536)
+  if (mc::env_lds_bytes(c.num_agents, TW, c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0,
+                        TW <= 4 ? 4 : 8) > 65536)
     return fail(MC_EINVAL, "per-env LDS window exceeds 64 KiB (numrobot / range / num_lasers too large)");
 
   Env* E = new Env();

@@ -84,7 +84,6 @@ struct Lds {
   int32_t *bx, *by;          // tile-block origin (tile units) of each agent
   Scal* sc;
   uint8_t* act;
-  uint32_t* obsrow;          // [N*Lc*E] E-bit crop rows
   WT* sink;                  // [64] target of lidar marks a lane does not make
 };
 
@@ -118,8 +117,6 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   q += 64;
   L.act = reinterpret_cast<uint8_t*>(q);
   q += ((size_t)s.N + 15) & ~(size_t)15;
-  L.obsrow = reinterpret_cast<uint32_t*>(q);
-  q += (((size_t)s.N * s.Lc * s.E * 4) + 15) & ~(size_t)15;
   L.sink = reinterpret_cast<WT*>(q);
   return L;
 }
@@ -299,6 +296,52 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
   }
   if (live) { L.x[C.sub] = x; L.y[C.sub] = y; }
   if (C.sub == 0) { L.sc->pen = pen; L.sc->moved = moved; }
+}
+
+// Same moves for a compile-time agent count NS <= 8: every lane of the slot
+// replays the robot-order loop on all robots' data in registers (no
+// cross-lane traffic); lane 0 publishes the result.
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT>& C, double pen_unit) {
+  const Lds<WT>& L = C.L;
+  int X[NS], Y[NS], DX[NS], DY[NS];
+  bool acts[NS], blk[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    X[i] = L.x0[i];
+    Y[i] = L.y0[i];
+    const int act = L.act[i];
+    acts[i] = act <= 3;  // not 0..3: no updateRobotPos call, no penalty
+    DX[i] = (act == 0) - (act == 2);
+    DY[i] = (act == 1) - (act == 3);
+    const int lx = X[i] + DX[i] - 8 * L.bx[i], ly = Y[i] + DY[i] - 8 * L.by[i];
+    blk[i] = (L.negr[i * (8 * s.TW + 1) + lx] >> ly) & (WT)1;
+  }
+  double pen = 0.0;
+  uint64_t moved = L.sc->moved;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int tx = X[i] + DX[i], ty = Y[i] + DY[i];
+    bool occ = false;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) occ |= X[j] == tx && Y[j] == ty;
+    const bool ok = acts[i] && !blk[i] && !occ;
+    if (ok) {
+      X[i] = tx;
+      Y[i] = ty;
+      moved |= 1ull << i;
+    }
+    if (acts[i] && !ok) pen += pen_unit;  // reward += -collision_penalty (:203)
+  }
+  if (C.sub == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      L.x[i] = X[i];
+      L.y[i] = Y[i];
+    }
+    L.sc->pen = pen;
+    L.sc->moved = moved;
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -672,63 +715,94 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
 
 // --------------------------------------------------------------------------
 // obs (dec_grid_rl.py:312-372): layer 0 robot_pad, 1 own free, 2 own obst,
-// E x E around each robot.  Each (agent, layer, row) becomes one E-bit word
-// in LDS; the uint8 output is then written as dwords.
+// E x E around each robot, uint8 [N][Lc][E][E] per env.  A lane builds four
+// consecutive E-bit crop rows in registers: their 4E bytes are exactly E
+// dwords of the output (each dword = 4 bits spread to bytes by a multiply).
 // --------------------------------------------------------------------------
-template <int NT, int EPW, typename WT>
-__device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>& C,
-                                          uint8_t* obs_out) {
-  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
-  const Lds<WT>& L = C.L;
-  const int N = s.N, E = s.E, ego = s.ego, Lc = s.Lc, TW = s.TW;
-  const uint64_t moved = L.sc->moved;
-  const uint64_t emask = low_mask(E);
-  for (int idx = C.sub; idx < N * Lc * E; idx += LPE) {
-    const int a = udiv(idx, s.mg_LcE), rem = idx - a * (Lc * E);
-    const int layer = udiv(rem, s.mg_E), r = rem - layer * E;
-    const int xa = L.x[a], ya = L.y[a];
+// Robot cells for the robot_pad layer: registers when the agent count is a
+// compile-time constant NS <= 8, LDS otherwise.
+template <int NS>
+struct Robots {
+  int x[NS > 0 ? NS : 1], y[NS > 0 ? NS : 1];
+};
+
+template <typename WT, int NS>
+__device__ __forceinline__ uint64_t obs_row(const State& s, const Lds<WT>& L, const Robots<NS>& R,
+                                            uint64_t moved, int row) {
+  const int E = s.E, ego = s.ego, Lc = s.Lc, TW = s.TW;
+  const int a = udiv(row, s.mg_LcE), rem = row - a * (Lc * E);
+  const int layer = udiv(rem, s.mg_E), r = rem - layer * E;
+  const int xa = L.x[a], ya = L.y[a];
+  if (layer == 0) {
+    const int cx = xa - ego + r, cy0 = ya - ego;
     uint64_t bits = 0;
-    if (layer == 0) {
-      const int cx = xa - ego + r, cy0 = ya - ego;
+    if constexpr (NS > 0) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const int dc = R.y[j] - cy0;
+        const bool on = ((moved >> j) & 1) && R.x[j] == cx && dc >= 0 && dc < E;
+        bits |= on ? (1ull << dc) : 0ull;
+      }
+    } else {
       for (uint64_t m = moved; m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
         const int dc = L.y[j] - cy0;
         if (L.x[j] == cx && dc >= 0 && dc < E) bits |= 1ull << dc;
       }
-    } else if (layer <= 2) {
-      // crop row = bits [ly0, ly0+E) of block row lx, gathered from the
-      // row's byte in consecutive tiles of the block
-      const int lx = xa - ego + r - 8 * L.bx[a];
-      const int ly0 = ya - ego - 8 * L.by[a];
-      const uint64_t* plane = layer == 1 ? L.fold : L.oold;
-      const int t0 = (a * TW + (lx >> 3)) * TW + (ly0 >> 3);
-      const int sh = (lx & 7) * 8;
-      const int nt = ((ly0 & 7) + E + 7) >> 3;
-      uint64_t acc = 0;
-      for (int q = 0; q < nt; ++q) acc |= ((plane[t0 + q] >> sh) & 0xFFull) << (8 * q);
-      bits = (acc >> (ly0 & 7)) & emask;
     }
-    L.obsrow[idx] = (uint32_t)bits;
+    return bits;
   }
-  __syncthreads();
-  const int total = N * Lc * E * E;
-  uint8_t* dst = obs_out + (size_t)C.e * total;
-  if ((total & 3) == 0) {
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-    for (int i = C.sub; i < total / 4; i += LPE) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = 4 * i + j;
-        const int row = udiv(q, s.mg_E), col = q - row * E;
-        v |= ((L.obsrow[row] >> col) & 1u) << (8 * j);
-      }
-      d32[i] = v;
-    }
+  // layers 1, 2: crop row = bits [ly0, ly0+E) of block row lx, gathered from
+  // the row's byte in consecutive tiles of the block
+  const int lx = xa - ego + r - 8 * L.bx[a];
+  const int ly0 = ya - ego - 8 * L.by[a];
+  const uint64_t* plane = layer == 1 ? L.fold : L.oold;
+  const int t0 = (a * TW + (lx >> 3)) * TW + (ly0 >> 3);
+  const int sh = (lx & 7) * 8;
+  uint64_t acc;
+  if (E <= 9) {  // at most two tiles; a second byte past the crop is masked off
+    acc = ((plane[t0] >> sh) & 0xFFull) | (((plane[t0 + 1] >> sh) & 0xFFull) << 8);
   } else {
-    for (int q = C.sub; q < total; q += LPE) {
-      const int row = udiv(q, s.mg_E), col = q - row * E;
-      dst[q] = (uint8_t)((L.obsrow[row] >> col) & 1u);
+    const int nt = ((ly0 & 7) + E + 7) >> 3;
+    acc = 0;
+    for (int q = 0; q < nt; ++q) acc |= ((plane[t0 + q] >> sh) & 0xFFull) << (8 * q);
+  }
+  return (acc >> (ly0 & 7)) & low_mask(E);
+}
+
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>& C,
+                                          uint8_t* obs_out) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  const int E = s.E;
+  const int rows = s.N * s.Lc * E;
+  const uint64_t moved = L.sc->moved;
+  Robots<NS> R;
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      R.x[j] = L.x[j];
+      R.y[j] = L.y[j];
+    }
+  }
+  uint8_t* dst = obs_out + (size_t)C.e * rows * E;
+  const bool dwords = E <= 16 && ((rows * E) & 3) == 0;  // every env's obs 4-byte aligned
+  for (int g = C.sub; 4 * g < rows; g += LPE) {
+    const int r0 = 4 * g;
+    if (r0 + 4 <= rows && dwords) {
+      uint64_t row[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[i] = obs_row<WT, NS>(s, L, R, moved, r0 + i);
+      const uint64_t cat = row[0] | (row[1] << E) | (row[2] << (2 * E)) | (row[3] << (3 * E));
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (size_t)r0 * E);  // 4E-byte aligned
+      for (int d = 0; d < E; ++d)
+        d32[d] = ((uint32_t)(cat >> (4 * d)) & 0xFu) * 0x00204081u & 0x01010101u;
+    } else {
+      for (int i = r0; i < rows && i < r0 + 4; ++i) {
+        const uint64_t bits = obs_row<WT, NS>(s, L, R, moved, i);
+        for (int c = 0; c < E; ++c) dst[(size_t)i * E + c] = (uint8_t)((bits >> c) & 1u);
+      }
     }
   }
 }
@@ -762,7 +836,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   const bool valid = e_raw < s.B;  // a short last workgroup leaves a slot idle
   C.e = valid ? e_raw : s.B - 1;
   const size_t slot_lds =
-      env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E, (int)sizeof(WT));
+      env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, (int)sizeof(WT));
   C.L = carve<WT>(smem + slot * slot_stride(slot_lds), s);
   const Lds<WT>& L = C.L;
   const int e = C.e;
@@ -809,7 +883,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     if (C.sub == 0) L.sc->numfree = s.numfree[L.sc->grid];
     __syncthreads();
     STAMP(2);
-    if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
+    if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
+    else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
     __syncthreads();
     STAMP(3);
     sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
@@ -867,7 +942,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   }
   STAMP(8);
 #if !(defined(MC_ABL) && MC_ABL == 5)
-  if (valid) write_obs<NT, EPW, WT>(s, C, obs_out);
+  if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
 #endif
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
@@ -905,8 +980,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
                       uint8_t* adj, int nt, int epw, hipStream_t stream) {
   const bool narrow = s.TW <= 4;  // window rows fit a u32
-  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, s.Lc, s.E,
-                                        narrow ? 4 : 8);
+  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, narrow ? 4 : 8);
 #define MC_LAUNCH_SH(T, P, W, SH)                                                              \
   hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + (P)-1) / (P)), dim3(T),             \
                      slot_stride(slot_lds) * (P), stream, s, mode, actions, env_mask, inj_pos,    \

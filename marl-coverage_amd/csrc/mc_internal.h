@@ -103,15 +103,13 @@ __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
 
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
 // rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
-__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int Lc, int E,
-                                                int rowbytes) {
+__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes) {
   size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
   b += (((size_t)3 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / fp / op rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
   b += (((size_t)N * 6 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by
   b += 64;                                             // scalars
   b += ((size_t)N + 15) & ~(size_t)15;                 // actions
-  b += (((size_t)N * Lc * E * 4) + 15) & ~(size_t)15;  // obs rows (E-bit words)
   b += 64 * (size_t)rowbytes;                          // per-lane sink words (lidar marks)
   return b;
 }
