@@ -140,6 +140,7 @@ def main():
     import torch.distributed as dist
 
     import marlcov
+    from marlcov.shards import aggregate_rate, rank_seeds, reduce_run
 
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -149,13 +150,14 @@ def main():
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
                maxsteps=args.maxsteps)
     N = c["numrobot"]
+    seeds = rank_seeds(rank)
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
-                                                    seed=1000 + rank, num_grids=B),
-                                   device=dev, seed=1 + rank, auto_reset=True)
+                                                    seed=seeds["grid_seed"], num_grids=B),
+                                   device=dev, seed=seeds["env_seed"], auto_reset=True)
     env.reset()
     K, W = args.steps, args.warmup
     g = torch.Generator(device=dev)
-    g.manual_seed(12345 + rank)
+    g.manual_seed(seeds["action_seed"])
     actions = torch.randint(0, 4, (W + K, B, N), dtype=torch.uint8, device=dev, generator=g)
     reward_sum = torch.zeros(B, dtype=torch.float64, device=dev)
     episodes = torch.zeros(B, dtype=torch.float64, device=dev)
@@ -222,14 +224,10 @@ def main():
     reward_sum += env.reward
     episodes += env.done.to(torch.float64)
     stats = torch.stack([reward_sum.sum(), episodes.sum()])
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(stats)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    stats, elapsed = reduce_run(stats, elapsed, world)
 
     n_gpus = world
-    value = B * n_gpus * K / elapsed
+    value = aggregate_rate(B, n_gpus, K, elapsed)
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"])
     achieved = bpe * B / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)

@@ -994,6 +994,10 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
   } else if (narrow) {
+    if (nt == 64 && getenv_spec() && ShapeC2::matches(s)) {
+      MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2);
+      return hipGetLastError();
+    }
     switch (nt) {
       case 64: MC_LAUNCH(64, 1, uint32_t); break;
       case 128: MC_LAUNCH(128, 1, uint32_t); break;
