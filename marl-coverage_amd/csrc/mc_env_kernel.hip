@@ -393,16 +393,20 @@ __device__ __forceinline__ void ray_advance(Ray& R, int k) {
 // nothing to mark ORs into its own sink word (no bank conflicts, no exec-mask
 // branches).  Re-marking an already free cell is harmless (OR).
 template <typename WT>
-__device__ __forceinline__ void ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT* sink) {
+// `dup`: the lane's previous ray (the adjacent beam) marks the same cell at
+// this step, so this one skips its atomic (near the robot adjacent beams share
+// cells: fewer same-address LDS atomics).  Returns whether the ray marked.
+__device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT* sink, bool dup) {
   const bool on = R.live && k <= R.K;
   const WT bit = (WT)1 << R.col;
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
 #if defined(MC_ABL) && MC_ABL == 1
   lds_or<WT>(sink, bit);  // timing ablation: no marks
 #else
-  lds_or<WT>(on ? (hit ? L.opr : L.fpr) + R.row : sink, bit);
+  lds_or<WT>((on && !dup) ? (hit ? L.opr : L.fpr) + R.row : sink, bit);
 #endif
   R.live = on && !hit;
+  return on;
 }
 
 template <int NT, int EPW, typename WT, int SUK>
@@ -433,6 +437,9 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
       // reads are all issued before its first mark, so no read waits behind
       // an LDS atomic (LDS ops complete in order).
       const int kmax = s.beam_kmax;
+      // dense beam sets: adjacent beams share cells for many steps (C4: 360
+      // beams, 1 degree apart); sparse ones only next to the robot
+      const bool dense = s.nbeams >= 64;
       for (int k0 = 1; k0 <= kmax; k0 += SU) {
         WT nr[SU][RPL];
         Ray q0[RPL];
@@ -453,9 +460,14 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
           if (k0 + u <= kmax) {
+            bool prev_on = false;
+            int prev_row = -1, prev_col = -1;
 #pragma unroll
             for (int j = 0; j < RPL; ++j) {
-              ray_mark<WT>(L, q[j], k0 + u, nr[u][j], sink);
+              const bool dup = dense && prev_on && q[j].row == prev_row && q[j].col == prev_col;
+              prev_row = q[j].row;
+              prev_col = q[j].col;
+              prev_on = ray_mark<WT>(L, q[j], k0 + u, nr[u][j], sink, dup);
               ray_advance(q[j], k0 + u);
             }
           }
