@@ -835,8 +835,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   using CtxT = Ctx<NT, EPW, WT>;
   constexpr int LPE = CtxT::LPE;
   constexpr int KI = CtxT::KI;
-  // march steps per batch: the whole march when the shape fixes beam_kmax
-  constexpr int SUK = SH::KM > 0 ? SH::KM : 8;
+  // march steps per batch: the whole march when the shape fixes a short
+  // beam_kmax, half of a long one (register pressure)
+  constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 1) / 2 : 8);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1001,6 +1002,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
 #define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
   using Dynamic = Shape<0, 0, 0, 0, 0>;
   using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
+  using ShapeC4 = Shape<8, 20, 360, 2, 20>; // 360 beams, R=20
   if (epw == 2) {
     if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
@@ -1018,6 +1020,10 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
       default: MC_LAUNCH(1024, 1, uint32_t); break;
     }
   } else {
+    if (nt == 256 && getenv_spec() && ShapeC4::matches(s)) {
+      MC_LAUNCH_SH(256, 1, uint64_t, ShapeC4);
+      return hipGetLastError();
+    }
     switch (nt) {
       case 64: MC_LAUNCH(64, 1, uint64_t); break;
       case 128: MC_LAUNCH(128, 1, uint64_t); break;
