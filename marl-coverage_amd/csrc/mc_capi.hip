@@ -23,6 +23,10 @@ int env_pack(const State& s);
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream);
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
+hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* obs,
+                           hipStream_t stream);
+size_t dijkstra_lds_bytes(const State& s, int pad);
+__global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
 }  // namespace mc
 
 namespace {
@@ -54,6 +58,7 @@ struct Env {
   int device = 0;
   int nt = 128;
   int epw = 1;  // envs per workgroup (2: two envs share one wave)
+  size_t dj_lds = 0;  // dijkstra_input: LDS bytes of the BFS kernel
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
   void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
@@ -156,8 +161,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     return fail(MC_EINVAL, "square sensor range must be >= 0");
   if (c.egoradius < 0) return fail(MC_EINVAL, "egoradius must be >= 0");
   if (c.pad < c.egoradius) return fail(MC_EINVAL, "pad must be >= egoradius");
-  if (c.dist_reward || c.dijkstra_input)
-    return fail(MC_EINVAL, "dist_reward / dijkstra_input obs layers are not in the HIP path yet");
+  if (c.dist_reward)
+    return fail(MC_EINVAL, "dist_reward obs layer / reward is not in the HIP path yet");
   if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
   if (c.maxsteps < 0) return fail(MC_EINVAL, "maxsteps must be >= 0");
 
@@ -202,7 +207,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.mg_TW2 = mc::magic_div((uint32_t)(TW * TW));
   s.ego = c.egoradius;
   s.E = 2 * c.egoradius + 1;
-  s.Lc = 3;
+  s.Lc = 3 + (c.dijkstra_input ? 1 : 0);
   s.mg_LcE = mc::magic_div((uint32_t)(s.Lc * s.E));
   s.mg_E = mc::magic_div((uint32_t)s.E);
   s.sensor = c.sensor_type;
@@ -276,6 +281,19 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) E->nt = v > E->nt ? v : E->nt;
   }
   E->epw = mc::env_pack(s);
+  if (c.dijkstra_input) {
+    // the BFS bitboards of one (env, agent) live in one workgroup's LDS
+    const size_t need = mc::dijkstra_lds_bytes(s, c.pad);
+    int maxlds = 0;
+    if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
+            hipSuccess ||
+        need + 1024 > (size_t)maxlds) {
+      mc_destroy(E);
+      return fail(MC_EINVAL, "dijkstra_input: %zu B of LDS bitboards for a %dx%d grid exceed the "
+                  "device's %d B per workgroup", need, c.width, c.length, maxlds);
+    }
+    E->dj_lds = need;
+  }
   mc_layout& L = E->lay;
   L.tile_rows = s.TR;
   L.tile_cols = s.TC;
@@ -435,6 +453,17 @@ int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {
   return MC_OK;
 }
 
+// dijkstra_input: obs layer 3 from the post-step maps (dec_grid_rl.py:354-358),
+// a second kernel on the same stream
+static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
+  if (!E->cfg.dijkstra_input) return MC_OK;
+  if (E->dj_lds > 65536)
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dijkstra_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dj_lds));
+  HIP_TRY(mc::launch_dijkstra(E->s, E->cfg.pad, 3, E->s.Lc, (uint8_t*)dev_obs, st));
+  return MC_OK;
+}
+
 static int ready(Env* E, const char* who) {
   if (!E->beams_set) return fail(MC_ESTATE, "%s: lidar beam table not set (mc_set_beam_table)", who);
   if (!E->grids_set) return fail(MC_ESTATE, "%s: grids not set (mc_set_grids / mc_generate_grids)", who);
@@ -450,7 +479,7 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, voi
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(mc::launch_env(E->s, mc::MODE_RESET, nullptr, dev_env_mask, dev_pos, nullptr, nullptr,
                          (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), (hipStream_t)stream));
-  return MC_OK;
+  return dijkstra_layer(E, dev_obs, (hipStream_t)stream);
 }
 
 int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
@@ -465,7 +494,7 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* 
   if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
   HIP_TRY(mc::launch_env(E->s, mc::MODE_STEP, dev_actions, nullptr, nullptr, dev_reward, dev_done,
                          (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), st));
-  return MC_OK;
+  return dijkstra_layer(E, dev_obs, st);
 }
 
 int64_t mc_field_bytes(void* env, int32_t f) {

@@ -764,6 +764,7 @@ __device__ __forceinline__ uint64_t obs_row(const State& s, const Lds<WT>& L, co
     }
     return bits;
   }
+  if (layer > 2) return 0;  // dijkstra layer: written by mc_dijkstra.hip
   // layers 1, 2: crop row = bits [ly0, ly0+E) of block row lx, gathered from
   // the row's byte in consecutive tiles of the block
   const int lx = xa - ego + r - 8 * L.bx[a];

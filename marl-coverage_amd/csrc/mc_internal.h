@@ -129,7 +129,8 @@ struct Shape {
   static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
-           (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) && (EGO_ == 0 || s.ego == EGO_) &&
+           (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
+           (EGO_ == 0 || (s.ego == EGO_ && s.Lc == 3)) &&
            (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_));
   }
 };

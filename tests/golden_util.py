@@ -108,6 +108,6 @@ def check_against_golden(env):
 
 
 def needs_layers(case):
-    """Golden cases using obs layers not in ABI v1 (dist_reward / dijkstra)."""
+    """Golden cases using the dist_reward layer / reward (not in the HIP path yet)."""
     c = case["meta"]["config"]
-    return bool(c.get("dist_reward")) or bool(c.get("dijkstra_input"))
+    return bool(c.get("dist_reward"))

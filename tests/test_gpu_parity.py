@@ -43,7 +43,7 @@ def test_facade_matches_reference_golden(torch_cuda, name):
     import marlcov
     case = load_case(name)
     if needs_layers(case):
-        pytest.skip("dist_reward / dijkstra obs layers are not in the HIP path yet (SURVEY 8f)")
+        pytest.skip("dist_reward layer / reward is not in the HIP path yet (SURVEY 8f)")
     env = make_env(marlcov.DecGridRL, case)
     replay(env, case, check_against_golden(env))
 
@@ -93,6 +93,16 @@ BATCH_CASES = {
                     lambda rs: bern(rs, 12, 12, 0.1), 4, 20),
     "n33_wide_window": (base_cfg(numrobot=33, sensor_config={"num_lasers": 7, "range": 3}),
                         lambda rs: bern(rs, 30, 30, 0.1), 2, 10),
+    # dijkstra_input obs layer: BFS path to the nearest
+    # unexplored cell; long episodes on small grids reach long paths
+    "dijkstra_square_r1": (base_cfg(numrobot=2, dijkstra_input=1, sensor_type="square_sensor",
+                                    sensor_config={"range": 1}, egoradius=2),
+                           lambda rs: bern(rs, 20, 20, 0.15), 8, 80),
+    "dijkstra_lidar_n3": (base_cfg(numrobot=3, dijkstra_input=1,
+                                   sensor_config={"num_lasers": 9, "range": 4}),
+                          lambda rs: tri(rs, 36, 28), 8, 60),
+    "dijkstra_c2_like": (base_cfg(numrobot=4, dijkstra_input=1), lambda rs: bern(rs, 128, 128, 0.1),
+                         4, 12),
 }
 
 
