@@ -36,17 +36,25 @@ CONFIGS = {
                desc="C2: 4 agents, 128x128 grid p_obst=0.1, lidar 21 beams R=10, egoradius 2"),
     "c4": dict(numrobot=8, width=256, sensor_config={"num_lasers": 360, "range": 20}, envs=8192,
                desc="C4: 8 agents, 256x256 grid p_obst=0.1, lidar 360 beams R=20, egoradius 2"),
+    # C2 with the dijkstra_input obs layer (BSA/BA*-style
+    # controllers); not a BASELINE metric config
+    "c2_dijkstra": dict(numrobot=4, width=128, sensor_config={"num_lasers": 21, "range": 10}, envs=4096,
+                        extra={"dijkstra_input": 1},
+                        desc="C2 + dijkstra_input obs layer (4 layers)"),
 }
 
 
-def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3):
+def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3, full_map_cells=0):
     """per agent s^2 (int8 grid window) + 4*ceil(s^2/8) (free and
     obst bit windows, read+write) + 2*ceil(s^2/8) (union window read+write) +
-    obs bytes + 1 (action) + 8 (position r/w); per env 32 B."""
+    obs bytes + 1 (action) + 8 (position r/w); per env 32 B.  Whole-map layers
+    (dijkstra_input; C5's distance map) add a read of the agent's free and obst
+    bit maps: 2*ceil(cells/8) per agent, as §8(d) prices C5."""
     s = 2 * math.ceil(beam_range) + 1
     bits = math.ceil(s * s / 8)
     obs = layers * (2 * ego + 1) ** 2
-    return n_agents * (s * s + 6 * bits + obs + 1 + 8) + 32
+    full = 2 * math.ceil(full_map_cells / 8) if full_map_cells else 0
+    return n_agents * (s * s + 6 * bits + obs + 1 + 8 + full) + 32
 
 
 # ---------------------------------------------------------------------------
@@ -61,7 +69,7 @@ def _cpu_worker(args):
 
     c = CONFIGS[cfgname]
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"],
-               allow_even_beams=True)
+               allow_even_beams=True, **c.get("extra", {}))
     rs = np.random.RandomState(1000 + seed)
     grid = rs.choice([1.0, -1.0], size=(c["width"], c["width"]), p=[0.9, 0.1])
     np.random.seed(seed)
@@ -148,7 +156,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
-               maxsteps=args.maxsteps)
+               maxsteps=args.maxsteps, **c.get("extra", {}))
     N = c["numrobot"]
     seeds = rank_seeds(rank)
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
@@ -228,7 +236,10 @@ def main():
 
     n_gpus = world
     value = aggregate_rate(B, n_gpus, K, elapsed)
-    bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"])
+    dj = bool(cfg.get("dijkstra_input"))
+    bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
+                                         layers=4 if dj else 3,
+                                         full_map_cells=(c["width"] + 2) ** 2 if dj else 0)
     achieved = bpe * B / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
     line = {
