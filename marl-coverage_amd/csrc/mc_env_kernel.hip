@@ -64,8 +64,7 @@ struct Scal {
   uint64_t moved;      // robots present in the reference's _robot_pad
   uint32_t cnt_free;   // newly set bits over all agents' free maps
   uint32_t cnt_vis;    // newly covered union cells (the obs reward)
-  uint32_t free_old, vis_old;
-  int32_t grid, numfree, currstep;
+  int32_t grid;
   uint32_t ep;
   int32_t do_reset;
   int32_t pad_;
@@ -155,8 +154,9 @@ struct Items {
   int a[KI];
   int gi[KI], gj[KI];   // global tile coordinates
   bool in[KI];          // tile inside the map (and item live)
-  uint64_t f[KI], o[KI], u[KI];     // old free / obst / union tiles
+  uint64_t f[KI], o[KI], u[KI];     // old free / obst / union tiles (raw loads)
   uint64_t nf[KI], no[KI], nu[KI];  // newly set bits
+  bool masks;                       // f / o / u were loaded (else known zero)
 };
 
 template <typename WT>
@@ -169,14 +169,13 @@ __device__ __forceinline__ void lds_or(WT* p, WT v) {
 // stage: one round trip for every staged tile (masks known zero after reset)
 // --------------------------------------------------------------------------
 template <int NT, int EPW, typename WT, int KI>
-__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, bool load_masks,
-                                      Items<KI>& I) {
+__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, int g,
+                                      bool load_masks, Items<KI>& I) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   const int items = s.N * TW2;
   const size_t mt = (size_t)s.TR * s.TC;
-  const int g = L.sc->grid;
   const uint64_t* gn = s.grid_neg + (size_t)g * mt;
   const uint64_t* gp = s.grid_pos + (size_t)g * mt;
   const bool square = s.sensor == 1;
@@ -202,19 +201,27 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     fb[k] = ((size_t)C.e * s.N + a) * mt;
   }
   const size_t vb = (size_t)C.e * mt;
+  // grid tiles first: the moves and the march need only them, so the mask
+  // tiles (needed from the merge on) stay in flight meanwhile (loads return
+  // in order; the compiler waits only for what each use needs)
 #pragma unroll
-  for (int k = 0; k < KI; ++k) {
-    n[k] = gn[gt[k]];
-    if (load_masks) {
-      I.f[k] = s.freem[fb[k] + gt[k]];
-      I.o[k] = s.obstm[fb[k] + gt[k]];
-      I.u[k] = s.vis[vb + gt[k]];
-    }
-  }
+  for (int k = 0; k < KI; ++k) n[k] = gn[gt[k]];
   if (square) {
 #pragma unroll
     for (int k = 0; k < KI; ++k) p[k] = gp[gt[k]];
   }
+  if (load_masks) {
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      I.f[k] = s.freem[fb[k] + gt[k]];
+      I.o[k] = s.obstm[fb[k] + gt[k]];
+      I.u[k] = s.vis[vb + gt[k]];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KI; ++k) I.f[k] = I.o[k] = I.u[k] = 0;
+  }
+  I.masks = load_masks;
   if (!square) {  // lidar mark rows start empty
     for (int r = C.sub; r < s.N * (8 * TW + 1); r += LPE) {
       L.fpr[r] = 0;
@@ -230,24 +237,46 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const bool in = I.in[k];
-    const bool m = load_masks && in;
-    I.f[k] = m ? I.f[k] : 0;  // outside the map: blocked (isInBounds), no marks
-    I.o[k] = m ? I.o[k] : 0;
-    I.u[k] = m ? I.u[k] : 0;
     const int idx = C.sub + k * LPE;
     if (idx < items) {
-      const uint64_t nt = in ? n[k] : ~0ull;
+      const uint64_t nt = in ? n[k] : ~0ull;  // outside the map: blocked (isInBounds)
       if (square) {
         L.neg[idx] = nt;
         L.pos[idx] = in ? p[k] : 0ull;
       }
-      L.fold[idx] = I.f[k];
-      L.oold[idx] = I.o[k];
       // scatter the tile's 8 row bytes into the row plane (byte tj of rows
       // 8*ti .. 8*ti+7 of the agent's block)
       uint8_t* dst = nb + ((size_t)(I.a[k] * (8 * TW + 1) + 8 * ti[k]) * sizeof(WT) + tj[k]);
 #pragma unroll
       for (int r = 0; r < 8; ++r) dst[r * sizeof(WT)] = (uint8_t)(nt >> (8 * r));
+    }
+  }
+}
+
+// old mask tiles of item k (zero outside the map, where nothing is stored)
+template <int KI>
+__device__ __forceinline__ void old_tiles(const Items<KI>& I, int k, uint64_t& f, uint64_t& o,
+                                          uint64_t& u) {
+  const bool m = I.masks && I.in[k];
+  f = m ? I.f[k] : 0;
+  o = m ? I.o[k] : 0;
+  u = m ? I.u[k] : 0;
+}
+
+// the old free / obstacle tiles into LDS (obs of an env that does not step)
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void stage_fold(const State& s, const Ctx<NT, EPW, WT>& C,
+                                           const Items<KI>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const int items = s.N * s.TW * s.TW;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = C.sub + k * LPE;
+    if (idx < items) {
+      uint64_t f, o, u;
+      old_tiles<KI>(I, k, f, o, u);
+      C.L.fold[idx] = f;
+      C.L.oold[idx] = o;
     }
   }
 }
@@ -554,12 +583,16 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
     I.nf[k] = I.no[k] = I.nu[k] = 0;
     if (idx < items) {
       const uint64_t fp = L.fp[idx], op = L.op[idx];
-      I.nf[k] = fp & ~I.f[k];
-      I.no[k] = op & ~I.o[k];
-      L.fold[idx] = I.f[k] | fp;
-      L.oold[idx] = I.o[k] | op;
+      uint64_t f0, o0, u0;
+      old_tiles<KI>(I, k, f0, o0, u0);  // first use of the mask loads
+      I.f[k] = f0;
+      I.o[k] = o0;
+      I.nf[k] = fp & ~f0;
+      I.no[k] = op & ~o0;
+      L.fold[idx] = f0 | fp;
+      L.oold[idx] = o0 | op;
       cf += __popcll(I.nf[k]);
-      uint64_t cand = fp & ~I.u[k];
+      uint64_t cand = fp & ~u0;
       const int a = I.a[k], gi = I.gi[k], gj = I.gj[k];
 #if defined(MC_ABL) && MC_ABL == 4
       for (int b = 0; b < 0; ++b) {  // timing ablation: no dedup
@@ -713,7 +746,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   Items<KI> I;
-  stage<NT, EPW, WT, KI>(s, C, /*load_masks=*/false, I);
+  stage<NT, EPW, WT, KI>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
   sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
   store_tiles<NT, EPW, WT, KI>(s, C, I);
@@ -856,45 +889,66 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   const int e = C.e;
 
   const bool is_step = mode == MODE_STEP;
-  const bool sentinel = valid && is_step && actions[(size_t)e * N] == 255;
-  const bool reset_req = valid && !is_step && (env_mask == nullptr || env_mask[e] != 0);
-  const bool active = valid && is_step && !sentinel;
 
   STAMP(0);
-  // ---- round trip 1: positions, actions, scalars, beam table ---------------
+  // ---- round trip 1: positions, actions, scalars, beam table.  Every load
+  // is issued (unpredicated, clamped addresses) before any result is used:
+  // one round trip, not one per branch.
+  const int ag = C.sub < N ? C.sub : 0;
+  // absent inputs read a harmless valid byte instead (no branch, no wait)
+  const uint8_t* ab = is_step ? actions + (size_t)e * N : reinterpret_cast<const uint8_t*>(s.pos);
+  const uint8_t* mb = env_mask != nullptr ? env_mask + e : reinterpret_cast<const uint8_t*>(s.pos);
+  const int2 p0 = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + ag];
+  const int act_raw = ab[ag], act0_raw = ab[0], req_raw = mb[0];
+  const int g0 = s.env_grid[e];
+  const uint64_t moved0 = s.moved[e];
+  const uint32_t free_old = s.free_cnt[e], vis_old = s.vis_cnt[e];
+  const int currstep0 = s.currstep[e];
+  const double dthresh0 = s.done_thresh[e];
+  const bool lidar = s.sensor == 0;
+  const int nbl = lidar ? s.nbeams : 1;  // a square env reads a dummy record
+  const int4 bm0 = reinterpret_cast<const int4*>(lidar ? (const void*)s.beams : (const void*)s.pos)
+      [C.sub < nbl ? C.sub : 0];
+  // every result is needed below: keep the compiler from sinking a load into
+  // the branch that uses it (that would make it a round trip of its own)
+  asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(act_raw), "v"(act0_raw), "v"(req_raw), "v"(g0),
+               "v"(bm0.x), "v"(bm0.w));
+  const int act = is_step ? act_raw : 255;
+  const int act0 = is_step ? act0_raw : 0;      // agent 0's byte: the sentinel
+  const int req = env_mask != nullptr ? req_raw : 1;
+
+  const bool sentinel = valid && is_step && act0 == 255;
+  const bool reset_req = valid && !is_step && req != 0;
+  const bool active = valid && is_step && !sentinel;
   if (C.sub < N) {
-    const int2 p = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + C.sub];
-    set_agent<WT>(s, L, C.sub, p.x, p.y);
-    if (active) L.act[C.sub] = actions[(size_t)e * N + C.sub];
+    set_agent<WT>(s, L, C.sub, p0.x, p0.y);
+    L.act[C.sub] = (uint8_t)act;
   }
   if (C.sub == 0) {
-    const int g = s.env_grid[e];
-    L.sc->grid = g;
-    L.sc->moved = s.moved[e];
+    L.sc->grid = g0;
+    L.sc->moved = moved0;
     L.sc->pen = 0.0;
     L.sc->cnt_free = 0;
     L.sc->cnt_vis = 0;
     L.sc->do_reset = 0;
-    if (active) {
-      L.sc->free_old = s.free_cnt[e];
-      L.sc->vis_old = s.vis_cnt[e];
-      L.sc->currstep = s.currstep[e];
-      L.sc->done_thresh = s.done_thresh[e];
-    }
   }
-  if (s.sensor == 0)
-    for (int b = C.sub; b < s.nbeams; b += LPE) L.beams[b] = s.beams[b];
+  if (lidar) {
+    if (C.sub < s.nbeams) reinterpret_cast<int4*>(L.beams)[C.sub] = bm0;
+    for (int b = C.sub + LPE; b < s.nbeams; b += LPE) L.beams[b] = s.beams[b];
+  }
   __syncthreads();
 
   if (active) {
     STAMP(1);
     Items<KI> I;
 #if defined(MC_ABL) && MC_ABL == 6
-    stage<NT, EPW, WT, KI>(s, C, false, I);  // timing ablation: grid tiles only
+    stage<NT, EPW, WT, KI>(s, C, g0, false, I);  // timing ablation: grid tiles only
 #else
-    stage<NT, EPW, WT, KI>(s, C, true, I);  // ---- round trip 2 ----
+    stage<NT, EPW, WT, KI>(s, C, g0, true, I);  // ---- round trip 2 ----
 #endif
-    if (C.sub == 0) L.sc->numfree = s.numfree[L.sc->grid];
+    // count_nonzero(grid > 0) for percent_covered: kept in a register until
+    // the reward (no wait here)
+    const int numfree = s.numfree[g0];
     __syncthreads();
     STAMP(2);
     if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
@@ -906,13 +960,13 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     STAMP(5);
     if (C.sub == 0) {
       Scal* c = L.sc;
-      const uint32_t fc = c->free_old + c->cnt_free;
-      const uint32_t vc = c->vis_old + c->cnt_vis;
-      const int cs = c->currstep + 1;                        // :154
+      const uint32_t fc = free_old + c->cnt_free;
+      const uint32_t vc = vis_old + c->cnt_vis;
+      const int cs = currstep0 + 1;                          // :154
       double r = c->pen;                                     // :120,132-145
       r += (double)c->cnt_vis;                               // :151,:256
-      const double pc = (double)fc / (double)c->numfree;     // :552
-      double dt = c->done_thresh;
+      const double pc = (double)fc / (double)numfree;        // :552
+      double dt = dthresh0;
       const double thr = (1.0 < dt) ? 1.0 : dt;              // min(done_thresh, 1)
       const bool covered = thr <= pc;
       if (covered) r += s.term;                              // :156-157
@@ -941,7 +995,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     // sentinel step / env left out of a partial reset: obs of the current
     // state only (dec_grid_rl.py:104-107,160)
     Items<KI> I;
-    stage<NT, EPW, WT, KI>(s, C, true, I);
+    stage<NT, EPW, WT, KI>(s, C, g0, true, I);
+    stage_fold<NT, EPW, WT, KI>(s, C, I);
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
