@@ -183,6 +183,14 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   if ((int64_t)c.num_agents * TW * TW > (int64_t)mc::kMaxItemsPerLane * 1024)
     return fail(MC_EINVAL, "numrobot * %d^2 window tiles = %d exceeds %d (range/egoradius too large)",
                 TW, c.num_agents * TW * TW, mc::kMaxItemsPerLane * 1024);
+  {
+    // the kernels index maps with 32-bit words and 24-bit factors
+    const int64_t tiles = (int64_t)((c.width + 7) / 8) * ((c.length + 7) / 8);
+    if ((int64_t)c.num_envs * c.num_agents * tiles >= ((int64_t)1 << 32) ||
+        (int64_t)c.num_envs * c.num_agents >= ((int64_t)1 << 24) || tiles >= ((int64_t)1 << 24))
+      return fail(MC_EINVAL, "num_envs * numrobot * map tiles = %lld exceeds 2^32 words per handle",
+                  (long long)c.num_envs * c.num_agents * tiles);
+  }
   if (TW > mc::kMaxWindowTiles)
     return fail(MC_EINVAL, "window half-width H = %d > 27 (range/egoradius too large)", H);
   if (mc::env_lds_bytes(c.num_agents, TW, c.sensor_type == MC_SENSOR_LIDAR ? c.num_beams : 0,

@@ -180,8 +180,11 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   const uint64_t* gp = s.grid_pos + (size_t)g * mt;
   const bool square = s.sensor == 1;
   uint64_t n[KI], p[KI];
-  size_t gt[KI], fb[KI];
+  // 32-bit word indices (mc_create bounds every map array below 2^32 words);
+  // products of 24-bit factors are single v_mul_u32_u24
+  uint32_t gt[KI], fw[KI];
   int ti[KI], tj[KI];
+  const uint32_t eN = (uint32_t)C.e * (uint32_t)s.N;
   // addresses first, then every load of the lane back to back with no
   // exec-mask branches (tiles outside the map read tile 0 and are replaced)
 #pragma unroll
@@ -196,11 +199,11 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     I.a[k] = a;
     I.gi[k] = gi;
     I.gj[k] = gj;
-    I.in[k] = it && gi >= 0 && gi < s.TR && gj >= 0 && gj < s.TC;
-    gt[k] = I.in[k] ? (size_t)gi * s.TC + gj : 0;
-    fb[k] = ((size_t)C.e * s.N + a) * mt;
+    I.in[k] = it & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
+    gt[k] = I.in[k] ? __umul24((uint32_t)gi, (uint32_t)s.TC) + (uint32_t)gj : 0u;
+    fw[k] = __umul24(eN + (uint32_t)a, (uint32_t)mt) + gt[k];
   }
-  const size_t vb = (size_t)C.e * mt;
+  const uint32_t vw = __umul24((uint32_t)C.e, (uint32_t)mt);
   // grid tiles first: the moves and the march need only them, so the mask
   // tiles (needed from the merge on) stay in flight meanwhile (loads return
   // in order; the compiler waits only for what each use needs)
@@ -213,9 +216,9 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   if (load_masks) {
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
-      I.f[k] = s.freem[fb[k] + gt[k]];
-      I.o[k] = s.obstm[fb[k] + gt[k]];
-      I.u[k] = s.vis[vb + gt[k]];
+      I.f[k] = s.freem[fw[k]];
+      I.o[k] = s.obstm[fw[k]];
+      I.u[k] = s.vis[vw + gt[k]];
     }
   } else {
 #pragma unroll
@@ -622,18 +625,18 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 template <int NT, int EPW, typename WT, int KI>
 __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, WT>& C,
                                             const Items<KI>& I) {
-  const size_t mt = (size_t)s.TR * s.TC;
+  const uint32_t mt = (uint32_t)(s.TR * s.TC);
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     if (!I.in[k]) continue;
-    const size_t gt = (size_t)I.gi[k] * s.TC + I.gj[k];
-    const size_t fb = ((size_t)C.e * s.N + I.a[k]) * mt + gt;
+    const uint32_t gt = __umul24((uint32_t)I.gi[k], (uint32_t)s.TC) + (uint32_t)I.gj[k];
+    const uint32_t fb = __umul24((uint32_t)C.e * (uint32_t)s.N + (uint32_t)I.a[k], mt) + gt;
     // only obstacle marks can fall on an edge tile's cells beyond the map
     const uint64_t no = I.no[k] & tile_in_grid(s, I.gi[k], I.gj[k]);
     if (I.nf[k]) s.freem[fb] = I.f[k] | I.nf[k];  // one writer per agent tile
     if (no) s.obstm[fb] = I.o[k] | no;
     if (I.nu[k])  // agents' blocks overlap: several lanes may add bits to one tile
-      atomicOr((unsigned long long*)(s.vis + (size_t)C.e * mt + gt), I.nu[k]);
+      atomicOr((unsigned long long*)(s.vis + (__umul24((uint32_t)C.e, mt) + gt)), I.nu[k]);
   }
 }
 
