@@ -836,22 +836,27 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>
     }
   }
   uint8_t* dst = obs_out + (size_t)C.e * rows * E;
-  const bool dwords = E <= 16 && ((rows * E) & 3) == 0;  // every env's obs 4-byte aligned
-  for (int g = C.sub; 4 * g < rows; g += LPE) {
-    const int r0 = 4 * g;
-    if (r0 + 4 <= rows && dwords) {
-      uint64_t row[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) row[i] = obs_row<WT, NS>(s, L, R, moved, r0 + i);
-      const uint64_t cat = row[0] | (row[1] << E) | (row[2] << (2 * E)) | (row[3] << (3 * E));
-      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (size_t)r0 * E);  // 4E-byte aligned
-      for (int d = 0; d < E; ++d)
+  // every env's obs 4-byte aligned and a whole number of 4-row groups
+  const bool dwords = E <= 16 && ((rows * E) & 3) == 0 && (rows & 3) == 0;
+  if (dwords) {
+    // lane q builds rows 2q, 2q+1; lanes 2m, 2m+1 swap them, so each holds the
+    // 4-row group m (4E bytes = E dwords) and writes half of its dwords
+    for (int q = C.sub; 2 * q < rows; q += LPE) {
+      const uint32_t two = (uint32_t)obs_row<WT, NS>(s, L, R, moved, 2 * q) |
+                           ((uint32_t)obs_row<WT, NS>(s, L, R, moved, 2 * q + 1) << E);
+      const uint32_t other = (uint32_t)__shfl_xor((int)two, 1);
+      const bool hi = q & 1;
+      const uint64_t cat = hi ? ((uint64_t)other | ((uint64_t)two << (2 * E)))
+                              : ((uint64_t)two | ((uint64_t)other << (2 * E)));
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (size_t)(2 * (q & ~1)) * E);
+      const int half = (E + 1) >> 1;
+      for (int d = hi ? half : 0; d < (hi ? E : half); ++d)
         d32[d] = ((uint32_t)(cat >> (4 * d)) & 0xFu) * 0x00204081u & 0x01010101u;
-    } else {
-      for (int i = r0; i < rows && i < r0 + 4; ++i) {
-        const uint64_t bits = obs_row<WT, NS>(s, L, R, moved, i);
-        for (int c = 0; c < E; ++c) dst[(size_t)i * E + c] = (uint8_t)((bits >> c) & 1u);
-      }
+    }
+  } else {
+    for (int i = C.sub; i < rows; i += LPE) {
+      const uint64_t bits = obs_row<WT, NS>(s, L, R, moved, i);
+      for (int c = 0; c < E; ++c) dst[(size_t)i * E + c] = (uint8_t)((bits >> c) & 1u);
     }
   }
 }
