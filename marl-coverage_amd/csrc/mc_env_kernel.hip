@@ -386,11 +386,13 @@ __device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT
 // (mc_set_beam_table rejects K > H).  Row planes: the cell's word is one add,
 // its bit one shift.
 // --------------------------------------------------------------------------
+// A ray's cell is packed as P = (row-plane byte offset << 6) | column: one
+// add advances it, P >> 6 addresses the row word, and the shift amount of
+// 1 << P is taken mod the word width by the hardware.
 struct Ray {
   uint32_t bits;     // minor-move bit per step (K <= 31)
-  int row, col;      // current cell: row-plane index (agent base + lx), ly
-  int drow, dcol;    // major step
-  int mrow, mcol;    // minor step (when the step's bit is set)
+  uint32_t P;        // packed current cell
+  uint32_t d0, d1;   // packed major step / minor step (added when the bit is set)
   int K;
   bool live;
 };
@@ -403,39 +405,44 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   const int b = R.live ? idx - a * s.nbeams : 0;
   const Beam bm = L.beams[b];
   const int xa = L.x[a], ya = L.y[a];
-  R.row = a * (8 * s.TW + 1) + xa - 8 * L.bx[a];
-  R.col = ya - 8 * L.by[a];
+  const int row = a * (8 * s.TW + 1) + xa - 8 * L.bx[a];
+  const int col = ya - 8 * L.by[a];
+  constexpr int RB = (int)sizeof(WT) * 64;  // one row in P units
+  R.P = ((uint32_t)row * RB) | (uint32_t)col;
   const bool ax = bm.axis == 0;
-  R.drow = ax ? bm.sign : 0;
-  R.dcol = ax ? 0 : bm.sign;
-  R.mrow = ax ? 0 : bm.msign;
-  R.mcol = ax ? bm.msign : 0;
+  R.d0 = (uint32_t)(ax ? bm.sign * RB : bm.sign);
+  R.d1 = (uint32_t)(ax ? bm.msign : bm.msign * RB);
   R.K = R.live ? bm.K : -1;
   R.bits = R.live ? (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0u;
   return R;
 }
 
 __device__ __forceinline__ void ray_advance(Ray& R, int k) {
-  const bool mv = (R.bits >> k) & 1u;
-  R.row += R.drow + (mv ? R.mrow : 0);
-  R.col += R.dcol + (mv ? R.mcol : 0);
+  const uint32_t m = 0u - ((R.bits >> k) & 1u);
+  R.P += R.d0 + (m & R.d1);
+}
+
+template <typename WT>
+__device__ __forceinline__ const WT* ray_word(const WT* plane, const Ray& R) {
+  return reinterpret_cast<const WT*>(reinterpret_cast<const char*>(plane) + (R.P >> 6));
 }
 
 // Branch-free mark: every lane issues one ds_or per ray and step; a lane with
 // nothing to mark ORs into its own sink word (no bank conflicts, no exec-mask
 // branches).  Re-marking an already free cell is harmless (OR).
-template <typename WT>
 // `dup`: the lane's previous ray (the adjacent beam) marks the same cell at
 // this step, so this one skips its atomic (near the robot adjacent beams share
 // cells: fewer same-address LDS atomics).  Returns whether the ray marked.
+template <typename WT>
 __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT* sink, bool dup) {
   const bool on = R.live && k <= R.K;
-  const WT bit = (WT)1 << R.col;
+  const WT bit = (WT)1 << (R.P & (8 * sizeof(WT) - 1));
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
 #if defined(MC_ABL) && MC_ABL == 1
   lds_or<WT>(sink, bit);  // timing ablation: no marks
 #else
-  lds_or<WT>((on && !dup) ? (hit ? L.opr : L.fpr) + R.row : sink, bit);
+  WT* tgt = const_cast<WT*>(ray_word<WT>(hit ? L.opr : L.fpr, R));
+  lds_or<WT>((on && !dup) ? tgt : sink, bit);
 #endif
   R.live = on && !hit;
   return on;
@@ -482,7 +489,7 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
           if (k0 + u <= kmax) {  // uniform
 #pragma unroll
             for (int j = 0; j < RPL; ++j) {
-              nr[u][j] = L.negr[q[j].row];
+              nr[u][j] = *ray_word<WT>(L.negr, q[j]);
               ray_advance(q[j], k0 + u);
             }
           }
@@ -493,12 +500,11 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
         for (int u = 0; u < SU; ++u) {
           if (k0 + u <= kmax) {
             bool prev_on = false;
-            int prev_row = -1, prev_col = -1;
+            uint32_t prev_p = 0xFFFFFFFFu;
 #pragma unroll
             for (int j = 0; j < RPL; ++j) {
-              const bool dup = dense && prev_on && q[j].row == prev_row && q[j].col == prev_col;
-              prev_row = q[j].row;
-              prev_col = q[j].col;
+              const bool dup = dense && prev_on && q[j].P == prev_p;
+              prev_p = q[j].P;
               prev_on = ray_mark<WT>(L, q[j], k0 + u, nr[u][j], sink, dup);
               ray_advance(q[j], k0 + u);
             }
@@ -878,8 +884,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   constexpr int LPE = CtxT::LPE;
   constexpr int KI = CtxT::KI;
   // march steps per batch: the whole march when the shape fixes a short
-  // beam_kmax, half of a long one (register pressure)
-  constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 1) / 2 : 8);
+  // beam_kmax, a quarter of a long one (register pressure)
+  constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
