@@ -284,13 +284,26 @@ __device__ __forceinline__ void stage_fold(const State& s, const Ctx<NT, EPW, WT
   }
 }
 
-// tile (ti, tj) of agent a gathered from a row plane (the inverse scatter)
+// tile (ti, tj) of agent a gathered from a row plane (the inverse scatter):
+// byte r of the tile = byte tj of row r0 + r
 template <typename WT>
 __device__ __forceinline__ uint64_t gather_tile(const WT* rows, int r0, int tj) {
-  uint64_t t = 0;
+  if constexpr (sizeof(WT) == 4) {
+    // v_perm_b32: two rows' byte tj into bytes 0, 1; then two such pairs
+    const uint32_t sel = (uint32_t)tj | ((uint32_t)(4 + tj) << 8) | 0x0C0C0000u;
+    uint32_t h[4];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) t |= (uint64_t)((rows[r0 + r] >> (8 * tj)) & (WT)0xFF) << (8 * r);
-  return t;
+    for (int q = 0; q < 4; ++q)
+      h[q] = __builtin_amdgcn_perm((uint32_t)rows[r0 + 2 * q + 1], (uint32_t)rows[r0 + 2 * q], sel);
+    const uint32_t lo = __builtin_amdgcn_perm(h[1], h[0], 0x05040100u);
+    const uint32_t hi = __builtin_amdgcn_perm(h[3], h[2], 0x05040100u);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+  } else {
+    uint64_t t = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) t |= (uint64_t)((rows[r0 + r] >> (8 * tj)) & (WT)0xFF) << (8 * r);
+    return t;
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -606,7 +619,11 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 #if defined(MC_ABL) && MC_ABL == 4
       for (int b = 0; b < 0; ++b) {  // timing ablation: no dedup
 #else
-      for (int b = 0; b < a; ++b) {  // marks of lower-index agents in this tile
+      // marks of lower-index agents in this tile (bounded by N-1 so a
+      // compile-time N unrolls it: the reads of all b are then in flight)
+#pragma unroll
+      for (int b = 0; b < s.N - 1; ++b) {
+        if (b >= a) break;
 #endif
         int bxb, byb;
         if constexpr (EPW == 1) {
