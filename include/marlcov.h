@@ -19,10 +19,12 @@
  *   - One handle per (device, stream); a handle is not thread-safe.
  *   - Coordinates are in the PADDED grid (the reference pads every map with a
  *     -1 border, dec_grid_rl.py:471-472): x in [0, width), y in [0, length).
- *   - Bit maps (MC_FIELD_FREE/OBST/VISITED/GRID_*) are 8x8-cell tiles: uint64
- *     [...][tile_rows][tile_cols], bit 8*r + c of tile (ti, tj) = cell
- *     (8*ti + r, 8*tj + c).  Cells of edge tiles beyond the grid are set in
- *     GRID_NEG (out of bounds = blocked) and clear in every other map.
+ *   - Bit maps (MC_FIELD_FREE/OBST/VISITED/GRID_*) are 8x8-cell tiles, bit
+ *     8*r + c of tile (ti, tj) = cell (8*ti + r, 8*tj + c), grouped 4x4 into
+ *     128-byte blocks: uint64 [...][tile_rows/4][tile_cols/4][4][4], tile
+ *     (ti, tj) at block (ti/4, tj/4), slot (ti%4, tj%4).  Cells beyond the
+ *     grid (edge and padding tiles) are set in GRID_NEG (out of bounds =
+ *     blocked) and clear in every other map.
  */
 #ifndef MARLCOV_H
 #define MARLCOV_H
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 2
+#define MARLCOV_ABI_VERSION 3
 
 enum {
   MC_OK = 0,
@@ -91,14 +93,14 @@ typedef struct mc_config {
 
 /* Derived geometry (mc_query). */
 typedef struct mc_layout {
-  int32_t tile_rows;          /* ceil(width / 8)                              */
-  int32_t tile_cols;          /* ceil(length / 8)                             */
+  int32_t tile_rows;          /* ceil(width / 8) rounded up to a multiple of 4  */
+  int32_t tile_cols;          /* ceil(length / 8) rounded up to a multiple of 4 */
   int32_t window_half;        /* H = max(ceil(range), egoradius)              */
   int32_t window_tiles;       /* TW: tiles per side staged per agent          */
   int32_t obs_layers;         /* Lc (3 + dist_reward + dijkstra_input)        */
   int32_t obs_side;           /* E = 2*egoradius + 1                          */
   int64_t obs_bytes_per_env;  /* N*Lc*E*E (uint8 obs)                         */
-  int64_t mask_words_per_agent; /* tile_rows * tile_cols                      */
+  int64_t mask_words_per_agent; /* tile_rows * tile_cols (one map)            */
   int64_t state_bytes;        /* device bytes owned by the handle             */
 } mc_layout;
 
@@ -106,9 +108,9 @@ typedef struct mc_layout {
 enum {
   MC_FIELD_POS = 0,          /* int32 [B][N][2] (x, y)                         */
   MC_FIELD_MOVED = 1,        /* uint64 [B]  bit i: robot i is in robot_pad     */
-  MC_FIELD_FREE = 2,         /* uint64 [B][N][tile_rows][tile_cols] _free_pad  */
-  MC_FIELD_OBST = 3,         /* uint64 [B][N][tile_rows][tile_cols] _obst_pad  */
-  MC_FIELD_VISITED = 4,      /* uint64 [B][tile_rows][tile_cols]    _visited   */
+  MC_FIELD_FREE = 2,         /* uint64 [B][N][map] _free_pad (map: see above)  */
+  MC_FIELD_OBST = 3,         /* uint64 [B][N][map] _obst_pad                   */
+  MC_FIELD_VISITED = 4,      /* uint64 [B][map]    _visited                    */
   MC_FIELD_FREE_COUNT = 5,   /* uint32 [B]  count_nonzero(_free_pad > 0)       */
   MC_FIELD_VISITED_COUNT = 6,/* uint32 [B]  sum(_visited)                      */
   MC_FIELD_CURRSTEP = 7,     /* int32  [B]  _currstep                          */
@@ -116,8 +118,8 @@ enum {
   MC_FIELD_ENV_GRID = 9,     /* int32  [B]  grid pool index of each env        */
   MC_FIELD_EPISODE = 10,     /* uint32 [B]  resets so far (RNG counter)        */
   MC_FIELD_NUMFREE = 11,     /* int32  [G]  count_nonzero(grid > 0) per grid   */
-  MC_FIELD_GRID_NEG = 12,    /* uint64 [G][tile_rows][tile_cols] grid < 0      */
-  MC_FIELD_GRID_POS = 13,    /* uint64 [G][tile_rows][tile_cols] grid > 0      */
+  MC_FIELD_GRID_NEG = 12,    /* uint64 [G][map] grid < 0                       */
+  MC_FIELD_GRID_POS = 13,    /* uint64 [G][map] grid > 0                       */
   MC_FIELD_COUNT = 14
 };
 

@@ -234,7 +234,7 @@ class BatchCoverageEnv:
     # ------------------------------------------------------------------
     def field_shape(self, field):
         B, N, G = self.num_envs, self.num_agents, self.num_grids
-        mw = (self.tile_rows, self.tile_cols)  # 8x8-cell tiles (tiles.py)
+        mw = (self.tile_rows // 4, self.tile_cols // 4, 4, 4)  # 4x4 blocks of 8x8-cell tiles (tiles.py)
         return {
             _lib.FIELD_POS: (B, N, 2), _lib.FIELD_MOVED: (B,), _lib.FIELD_FREE: (B, N) + mw,
             _lib.FIELD_OBST: (B, N) + mw, _lib.FIELD_VISITED: (B,) + mw, _lib.FIELD_FREE_COUNT: (B,),

@@ -74,7 +74,7 @@ struct FieldDesc {
 
 FieldDesc field(Env* E, int f) {
   const mc::State& s = E->s;
-  const int64_t B = s.B, N = s.N, mw = (int64_t)s.TR * s.TC, G = s.G;
+  const int64_t B = s.B, N = s.N, mw = s.MT, G = s.G;
   switch (f) {
     case MC_FIELD_POS: return {s.pos, B * N * 2 * 4};
     case MC_FIELD_MOVED: return {s.moved, B * 8};
@@ -185,7 +185,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
                 TW, c.num_agents * TW * TW, mc::kMaxItemsPerLane * 1024);
   {
     // the kernels index maps with 32-bit words and 24-bit factors
-    const int64_t tiles = (int64_t)((c.width + 7) / 8) * ((c.length + 7) / 8);
+    const int64_t tiles = (int64_t)(((c.width + 7) / 8 + 3) / 4) * (((c.length + 7) / 8 + 3) / 4) * 16;
     if ((int64_t)c.num_envs * c.num_agents * tiles >= ((int64_t)1 << 32) ||
         (int64_t)c.num_envs * c.num_agents >= ((int64_t)1 << 24) || tiles >= ((int64_t)1 << 24))
       return fail(MC_EINVAL, "num_envs * numrobot * map tiles = %lld exceeds 2^32 words per handle",
@@ -208,6 +208,9 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.Lp = c.length;
   s.TR = (c.width + 7) / 8;
   s.TC = (c.length + 7) / 8;
+  s.TRS = (s.TR + 3) / 4;
+  s.TCS = (s.TC + 3) / 4;
+  s.MT = s.TRS * s.TCS * 16;
   s.G = c.num_grids;
   s.H = H;
   s.TW = TW;
@@ -237,7 +240,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     delete E;
     return fail(MC_EHIP, "hipSetDevice(%d): %s", hip_device, hipGetErrorString(he));
   }
-  const size_t B = s.B, N = s.N, mw = (size_t)s.TR * s.TC, G = s.G;
+  const size_t B = s.B, N = s.N, mw = (size_t)s.MT, G = s.G;
   void* p = nullptr;
   int rc = MC_OK;
   size_t total = 0;
@@ -303,8 +306,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->dj_lds = need;
   }
   mc_layout& L = E->lay;
-  L.tile_rows = s.TR;
-  L.tile_cols = s.TC;
+  L.tile_rows = 4 * s.TRS;
+  L.tile_cols = 4 * s.TCS;
   L.window_half = s.H;
   L.window_tiles = s.TW;
   L.obs_layers = s.Lc;

@@ -36,7 +36,7 @@ __device__ __forceinline__ int tile_bit(int r, int c) { return ((r & 7) << 3) | 
 // isInBounds + grid < 0 (dec_grid_rl.py:284-295, :310) read from HBM
 __device__ __forceinline__ bool grid_blocked(const State& s, int g, int x, int y) {
   if (x < 0 || y < 0 || x >= s.Wp || y >= s.Lp) return true;
-  const uint64_t t = s.grid_neg[((size_t)g * s.TR + (x >> 3)) * s.TC + (y >> 3)];
+  const uint64_t t = s.grid_neg[(size_t)g * s.MT + tile_index(s.TCS, x >> 3, y >> 3)];
   return (t >> tile_bit(x, y)) & 1ull;
 }
 

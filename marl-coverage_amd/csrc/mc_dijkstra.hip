@@ -45,7 +45,7 @@ __device__ __forceinline__ void row_word(const State& s, const DjLds& L, int pad
   const int tj0 = Y0 < 0 ? 0 : (Y0 >> 3), tj1 = min((Y0 + 63) >> 3, s.TC - 1);
   const int sh = (X & 7) * 8;
   for (int tj = tj0; tj <= tj1; ++tj) {
-    const int t = (X >> 3) * s.TC + tj;
+    const int t = (int)tile_index(s.TCS, X >> 3, tj);
     const uint64_t fb = (L.tf[t] >> sh) & 0xFFull, obb = (L.to[t] >> sh) & 0xFFull;
     const int off = 8 * tj - Y0;  // bit position of the tile's column 0
     if (off >= 0) {
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kDjThreads) void dijkstra_kernel(State s, int pad, 
   const int e = blockIdx.x / s.N, a = blockIdx.x - e * s.N;
   const int tid = threadIdx.x;
   const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6, NW = RX * RW;
-  const int mt = s.TR * s.TC;
+  const int mt = s.MT;
   DjLds L;
   uint64_t* p = reinterpret_cast<uint64_t*>(smem);
   L.ob = p;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kDjThreads) void dijkstra_kernel(State s, int pad, 
 
 size_t dijkstra_lds_bytes(const State& s, int pad) {
   const size_t RX = s.Wp + 2 * pad, RW = (s.Lp + 2 * pad + 63) / 64;
-  return (7 * RX * RW + 2 * (size_t)s.TR * s.TC) * 8;
+  return (7 * RX * RW + 2 * (size_t)s.MT) * 8;
 }
 
 hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* obs,

@@ -175,7 +175,7 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   const int items = s.N * TW2;
-  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t mt = (size_t)s.MT;
   const uint64_t* gn = s.grid_neg + (size_t)g * mt;
   const uint64_t* gp = s.grid_pos + (size_t)g * mt;
   const bool square = s.sensor == 1;
@@ -200,7 +200,7 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     I.gi[k] = gi;
     I.gj[k] = gj;
     I.in[k] = it & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
-    gt[k] = I.in[k] ? __umul24((uint32_t)gi, (uint32_t)s.TC) + (uint32_t)gj : 0u;
+    gt[k] = I.in[k] ? tile_index(s.TCS, gi, gj) : 0u;
     fw[k] = __umul24(eN + (uint32_t)a, (uint32_t)mt) + gt[k];
   }
   const uint32_t vw = __umul24((uint32_t)C.e, (uint32_t)mt);
@@ -648,11 +648,11 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 template <int NT, int EPW, typename WT, int KI>
 __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, WT>& C,
                                             const Items<KI>& I) {
-  const uint32_t mt = (uint32_t)(s.TR * s.TC);
+  const uint32_t mt = (uint32_t)s.MT;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     if (!I.in[k]) continue;
-    const uint32_t gt = __umul24((uint32_t)I.gi[k], (uint32_t)s.TC) + (uint32_t)I.gj[k];
+    const uint32_t gt = tile_index(s.TCS, I.gi[k], I.gj[k]);
     const uint32_t fb = __umul24((uint32_t)C.e * (uint32_t)s.N + (uint32_t)I.a[k], mt) + gt;
     // only obstacle marks can fall on an edge tile's cells beyond the map
     const uint64_t no = I.no[k] & tile_in_grid(s, I.gi[k], I.gj[k]);
@@ -723,7 +723,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   __syncthreads();
   const uint32_t ep = L.sc->ep;
   const int g = L.sc->grid;
-  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t mt = (size_t)s.MT;
   {  // zero this env's maps (:505-514)
     uint64_t* f = s.freem + (size_t)e * N * mt;
     uint64_t* o = s.obstm + (size_t)e * N * mt;

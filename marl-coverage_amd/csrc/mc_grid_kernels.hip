@@ -22,7 +22,7 @@ __global__ __launch_bounds__(64) void share_kernel(State s, const uint8_t* __res
   const int e = blockIdx.y;
   const int N = s.N;
   if (actions[(size_t)e * N] == 255) return;  // sentinel: no state change
-  const size_t mw = (size_t)s.TR * s.TC;
+  const size_t mw = (size_t)s.MT;
   const int lane = threadIdx.x;
   const size_t w = (size_t)blockIdx.x * 64 + lane;
   uint64_t* fo = reinterpret_cast<uint64_t*>(smem);   // [N][64]
@@ -66,13 +66,15 @@ __global__ __launch_bounds__(64) void share_kernel(State s, const uint8_t* __res
 // int8 [G][Wp][Lp] -> neg/pos tiles, numfree[g] = count(grid > 0).  Cells of
 // an edge tile beyond the grid are obstacles (isInBounds).
 __global__ void pack_grids_kernel(State s, const int8_t* __restrict__ grids) {
-  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t mt = (size_t)s.MT;
   const size_t total = (size_t)s.G * mt;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
     const int g = (int)(i / mt);
     const size_t rem = i - (size_t)g * mt;
-    const int ti = (int)(rem / s.TC), tj = (int)(rem - (size_t)ti * s.TC);
+    // tile_index inverse: 4x4-tile blocks, row-major
+    const int blk = (int)(rem >> 4), in = (int)(rem & 15);
+    const int ti = (blk / s.TCS) * 4 + (in >> 2), tj = (blk % s.TCS) * 4 + (in & 3);
     uint64_t neg = 0, pos = 0;
     for (int r = 0; r < 8; ++r) {
       const int x = 8 * ti + r;
@@ -95,13 +97,15 @@ __global__ void pack_grids_kernel(State s, const int8_t* __restrict__ grids) {
 // Utils/gridmaker.py:127-128, plus the np.pad of dec_grid_rl.py:471).  One
 // Philox block per tile row: 8 cells x 32 bits = 2 calls.
 __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int all_free) {
-  const size_t mt = (size_t)s.TR * s.TC;
+  const size_t mt = (size_t)s.MT;
   const size_t total = (size_t)s.G * mt;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
     const int g = (int)(i / mt);
     const size_t rem = i - (size_t)g * mt;
-    const int ti = (int)(rem / s.TC), tj = (int)(rem - (size_t)ti * s.TC);
+    // tile_index inverse: 4x4-tile blocks, row-major
+    const int blk = (int)(rem >> 4), in = (int)(rem & 15);
+    const int ti = (blk / s.TCS) * 4 + (in >> 2), tj = (blk % s.TCS) * 4 + (in & 3);
     uint64_t neg = 0;
     for (int r = 0; r < 8; ++r) {
       const int x = 8 * ti + r;
@@ -125,7 +129,7 @@ __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int al
 }
 
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream) {
-  const size_t mw = (size_t)s.TR * s.TC;
+  const size_t mw = (size_t)s.MT;
   dim3 grid((unsigned)((mw + 63) / 64), s.B), block(64);
   const size_t lds = (size_t)s.N * 64 * 16 + 64 * 8;
   hipLaunchKernelGGL(share_kernel, grid, block, lds, stream, s, actions);
@@ -133,14 +137,14 @@ hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stre
 }
 
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream) {
-  const size_t total = (size_t)s.G * s.TR * s.TC;
+  const size_t total = (size_t)s.G * s.MT;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   hipLaunchKernelGGL(pack_grids_kernel, dim3(blocks), dim3(256), 0, stream, s, grids);
   return hipGetLastError();
 }
 
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream) {
-  const size_t total = (size_t)s.G * s.TR * s.TC;
+  const size_t total = (size_t)s.G * s.MT;
   const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   double t = p * 4294967296.0;
   uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (t <= 0.0 ? 0u : (uint32_t)t);
