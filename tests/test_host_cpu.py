@@ -143,3 +143,26 @@ def test_bench_bytes_formula_matches_survey():
     assert bench.algorithmic_bytes_per_env_step(1, 10, 2) == 893
     assert bench.algorithmic_bytes_per_env_step(4, 10, 2) == 3476
     assert bench.algorithmic_bytes_per_env_step(8, 20, 2) == 24280
+
+
+def test_tile_block_layout_round_trip():
+    """marlcov.tiles mirrors the device map order (include/marlcov.h, ABI v3):
+    4x4 blocks of 8x8-cell tiles, tile_index = ((ti/4)*TCS + tj/4)*16 +
+    (ti%4)*4 + tj%4, bit 8*r + c = cell (8*ti + r, 8*tj + c)."""
+    import numpy as np
+    from marlcov.tiles import blocks_to_tiles, cells_to_tiles, tiles_to_cells
+    rng = np.random.default_rng(3)
+    cells = (rng.random((2, 3, 130, 70)) < 0.3).astype(np.uint8)
+    blocks = cells_to_tiles(cells, blocks=True)
+    assert blocks.shape == (2, 3, 5, 3, 4, 4) and blocks.dtype == np.uint64
+    np.testing.assert_array_equal(tiles_to_cells(blocks, 130, 70), cells)
+    grid = blocks_to_tiles(blocks)
+    flat = blocks.reshape(2, 3, -1)
+    tcs = blocks.shape[3]
+    for ti, tj in [(0, 0), (5, 7), (16, 8), (13, 3)]:
+        idx = ((ti >> 2) * tcs + (tj >> 2)) * 16 + (ti & 3) * 4 + (tj & 3)
+        assert flat[1, 2, idx] == grid[1, 2, ti, tj]
+        r, c = 3, 6
+        bit = (int(grid[1, 2, ti, tj]) >> (8 * r + c)) & 1
+        x, y = 8 * ti + r, 8 * tj + c
+        assert bit == (cells[1, 2, x, y] if x < 130 and y < 70 else 0)
