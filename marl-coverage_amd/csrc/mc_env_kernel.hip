@@ -225,12 +225,6 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     for (int k = 0; k < KI; ++k) I.f[k] = I.o[k] = I.u[k] = 0;
   }
   I.masks = load_masks;
-  if (!square) {  // lidar mark rows start empty
-    for (int r = C.sub; r < s.N * (8 * TW + 1); r += LPE) {
-      L.fpr[r] = 0;
-      L.opr[r] = 0;
-    }
-  }
 #ifdef MC_STAMPS
   STAMP(11);  // loads issued
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -281,6 +275,17 @@ __device__ __forceinline__ void stage_fold(const State& s, const Ctx<NT, EPW, WT
       C.L.fold[idx] = f;
       C.L.oold[idx] = o;
     }
+  }
+}
+
+// lidar mark rows start empty (LDS stores: issued while loads are in flight)
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  if (s.sensor != 0) return;
+  for (int r = C.sub; r < s.N * (8 * s.TW + 1); r += LPE) {
+    C.L.fpr[r] = 0;
+    C.L.opr[r] = 0;
   }
 }
 
@@ -772,6 +777,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   Items<KI> I;
+  zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
   sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
@@ -940,6 +946,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   const int nbl = lidar ? s.nbeams : 1;  // a square env reads a dummy record
   const int4 bm0 = reinterpret_cast<const int4*>(lidar ? (const void*)s.beams : (const void*)s.pos)
       [C.sub < nbl ? C.sub : 0];
+  zero_marks<NT, EPW, WT>(s, C);  // overlaps the round trip
   // every result is needed below: keep the compiler from sinking a load into
   // the branch that uses it (that would make it a round trip of its own)
   asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(act_raw), "v"(act0_raw), "v"(req_raw), "v"(g0),
