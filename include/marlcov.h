@@ -83,8 +83,8 @@ typedef struct mc_config {
   int32_t comm_radius;        /* 'comm_radius' (Chebyshev)                    */
   int32_t map_sharing;        /* 'map_sharing'                                */
   int32_t single_square_tool; /* 'single_square_tool'                         */
-  int32_t dist_reward;        /* 'dist_reward'   (must be 0: not in the HIP path yet) */
-  int32_t dijkstra_input;     /* 'dijkstra_input' (must be 0: not in the HIP path yet) */
+  int32_t dist_reward;        /* 'dist_reward' (float obs layer: mc_set_dist_obs) */
+  int32_t dijkstra_input;     /* 'dijkstra_input'                             */
   int32_t auto_reset;         /* batch extra: re-place agents on done         */
   int32_t reset_grid_mode;    /* 0: keep the env's grid on reset;
                                  1: draw a grid uniformly from the pool       */
@@ -174,6 +174,14 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward,
 int64_t mc_field_bytes(void* env, int32_t field);
 int mc_get_state(void* env, int32_t field, void* dev_dst, int64_t bytes, void* stream);
 int mc_set_state(void* env, int32_t field, const void* dev_src, int64_t bytes, void* stream);
+
+/* dist_reward (dec_grid_rl.py:222-223,239-240,260-282,350-352): register the
+ * caller's float32 [B][N][E][E] buffer that every mc_reset / mc_step fills
+ * with the distance-map crop (obs layer 3; the uint8 obs hold 0 there).
+ * Required before the first reset when cfg.dist_reward != 0.  With
+ * dijkstra_input as well, layer 3 of the uint8 obs is the dijkstra path and
+ * layer 4 is 0, as in the reference (the dist crop is overwritten, :354). */
+int mc_set_dist_obs(void* env, float* dev_dist_obs);
 
 /* Synchronise `stream` and report (then clear) the device error word. */
 int mc_check(void* env, void* stream);

@@ -90,6 +90,7 @@ SIGNATURES = [
     ("mc_set_state", ctypes.c_int, [_VP, _I32, _VP, _I64, _VP]),
     ("mc_check", ctypes.c_int, [_VP, _VP]),
     ("mc_debug_stamps", ctypes.c_int, [_VP, _VP]),
+    ("mc_set_dist_obs", ctypes.c_int, [_VP, _VP]),
 ]
 
 _lib = None

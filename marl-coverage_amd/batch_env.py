@@ -159,6 +159,13 @@ class BatchCoverageEnv:
         if want_adjacency is None:
             want_adjacency = bool(self.config.get("allow_comm", 0))
         self.adj = torch.zeros((B, N, N), dtype=torch.uint8, device=dev) if want_adjacency else None
+        # dist_reward: the float32 distance-map crop (obs layer 3), written by
+        # every reset / step next to the uint8 obs (include/marlcov.h)
+        self.dist_obs = None
+        if c.dist_reward:
+            E = lay.obs_side
+            self.dist_obs = torch.zeros((B, N, E, E), dtype=torch.float32, device=dev)
+            _lib.check(self.lib.mc_set_dist_obs(self._h, self.dist_obs.data_ptr()), "mc_set_dist_obs")
 
     # ------------------------------------------------------------------
     def _stream(self):

@@ -25,6 +25,10 @@ hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
 hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* obs,
                            hipStream_t stream);
+hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
+                       hipStream_t stream);
+size_t dist_lds_bytes(const State& s, int pad);
+__global__ void dist_kernel(State s, int pad, int post, float* pre_out, float* dist_obs);
 size_t dijkstra_lds_bytes(const State& s, int pad);
 __global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
 }  // namespace mc
@@ -59,6 +63,9 @@ struct Env {
   int nt = 128;
   int epw = 1;  // envs per workgroup (2: two envs share one wave)
   size_t dj_lds = 0;  // dijkstra_input: LDS bytes of the BFS kernel
+  size_t dt_lds = 0;  // dist_reward: LDS bytes of the distance kernel
+  float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
+  float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
   void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
@@ -161,8 +168,6 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     return fail(MC_EINVAL, "square sensor range must be >= 0");
   if (c.egoradius < 0) return fail(MC_EINVAL, "egoradius must be >= 0");
   if (c.pad < c.egoradius) return fail(MC_EINVAL, "pad must be >= egoradius");
-  if (c.dist_reward)
-    return fail(MC_EINVAL, "dist_reward obs layer / reward is not in the HIP path yet");
   if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
   if (c.maxsteps < 0) return fail(MC_EINVAL, "maxsteps must be >= 0");
 
@@ -218,7 +223,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.mg_TW2 = mc::magic_div((uint32_t)(TW * TW));
   s.ego = c.egoradius;
   s.E = 2 * c.egoradius + 1;
-  s.Lc = 3 + (c.dijkstra_input ? 1 : 0);
+  s.Lc = 3 + (c.dist_reward ? 1 : 0) + (c.dijkstra_input ? 1 : 0);
+  s.dist = c.dist_reward ? 1 : 0;
   s.mg_LcE = mc::magic_div((uint32_t)(s.Lc * s.E));
   s.mg_E = mc::magic_div((uint32_t)s.E);
   s.sensor = c.sensor_type;
@@ -304,6 +310,26 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
                   "device's %d B per workgroup", need, c.width, c.length, maxlds);
     }
     E->dj_lds = need;
+  }
+  if (c.dist_reward) {
+    const size_t need = mc::dist_lds_bytes(s, c.pad);
+    int maxlds = 0;
+    if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
+            hipSuccess ||
+        need + 4096 + 1024 > (size_t)maxlds) {
+      mc_destroy(E);
+      return fail(MC_EINVAL, "dist_reward: %zu B of LDS bitboards for a %dx%d grid exceed the "
+                  "device's %d B per workgroup", need, c.width, c.length, maxlds);
+    }
+    E->dt_lds = need;
+    void* q = nullptr;
+    if (dev_alloc(E, &q, (size_t)s.B * s.N * 8 * sizeof(float)) != MC_OK) {
+      std::string msg = g_err;
+      mc_destroy(E);
+      return fail(MC_EHIP, "%s", msg.c_str());
+    }
+    E->dist_pre = (float*)q;
+    E->s.dist_pre = E->dist_pre;
   }
   mc_layout& L = E->lay;
   L.tile_rows = 4 * s.TRS;
@@ -475,9 +501,22 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
   return MC_OK;
 }
 
+// dist_reward: the distance terms of the maps before sensing (PRE, read by
+// the env kernel's reward) or the obs layer of the maps after it (POST)
+static int dist_terms(Env* E, int post, hipStream_t st) {
+  if (!E->cfg.dist_reward) return MC_OK;
+  if (E->dt_lds > 65536)
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dist_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dt_lds));
+  HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, post, E->dist_pre, E->dist_obs, st));
+  return MC_OK;
+}
+
 static int ready(Env* E, const char* who) {
   if (!E->beams_set) return fail(MC_ESTATE, "%s: lidar beam table not set (mc_set_beam_table)", who);
   if (!E->grids_set) return fail(MC_ESTATE, "%s: grids not set (mc_set_grids / mc_generate_grids)", who);
+  if (E->cfg.dist_reward && !E->dist_obs)
+    return fail(MC_ESTATE, "%s: dist_reward needs the float obs buffer (mc_set_dist_obs)", who);
   return MC_OK;
 }
 
@@ -490,7 +529,9 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, voi
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(mc::launch_env(E->s, mc::MODE_RESET, nullptr, dev_env_mask, dev_pos, nullptr, nullptr,
                          (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), (hipStream_t)stream));
-  return dijkstra_layer(E, dev_obs, (hipStream_t)stream);
+  rc = dijkstra_layer(E, dev_obs, (hipStream_t)stream);
+  if (rc) return rc;
+  return dist_terms(E, 1, (hipStream_t)stream);
 }
 
 int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
@@ -503,9 +544,13 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* 
   hipStream_t st = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(E->device));
   if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
+  rc = dist_terms(E, 0, st);  // observe() reads the maps before sensing
+  if (rc) return rc;
   HIP_TRY(mc::launch_env(E->s, mc::MODE_STEP, dev_actions, nullptr, nullptr, dev_reward, dev_done,
                          (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), st));
-  return dijkstra_layer(E, dev_obs, st);
+  rc = dijkstra_layer(E, dev_obs, st);
+  if (rc) return rc;
+  return dist_terms(E, 1, st);
 }
 
 int64_t mc_field_bytes(void* env, int32_t f) {
@@ -536,6 +581,14 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (f == MC_FIELD_GRID_NEG || f == MC_FIELD_GRID_POS || f == MC_FIELD_NUMFREE) E->grids_set = true;
+  return MC_OK;
+}
+
+int mc_set_dist_obs(void* env, float* dev_dist_obs) {
+  Env* E = as_env(env);
+  if (!E || !dev_dist_obs) return fail(MC_EINVAL, "mc_set_dist_obs: null argument");
+  if (!E->cfg.dist_reward) return fail(MC_EINVAL, "mc_set_dist_obs: config has dist_reward = 0");
+  E->dist_obs = dev_dist_obs;
   return MC_OK;
 }
 

@@ -30,6 +30,12 @@ __device__ __forceinline__ uint32_t bounded(uint32_t r, uint32_t n) {
   return (uint32_t)(((uint64_t)r * n) >> 32);
 }
 
+// distance_map value (dec_grid_rl.py:260-282) of a cell at L1 distance d
+// when the map maximum is M, in the reference's float32 steps
+__device__ __forceinline__ float dist_value(float d, float M) {
+  return M > 0.0f ? __fsub_rn(1.0f, __fdiv_rn(d, M)) : __fsub_rn(1.0f, d);
+}
+
 // bit of cell (r, c) inside its 8x8 tile
 __device__ __forceinline__ int tile_bit(int r, int c) { return ((r & 7) << 3) | (c & 7); }
 

@@ -22,7 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "mc_device.h"
+#include "mc_bitboard.h"
 
 namespace mc {
 
@@ -34,29 +34,6 @@ struct DjLds {
   uint64_t *ob, *tg, *bl, *f0, *f1, *m0, *m1;
   uint64_t *tf, *to;  // the agent's free / obstacle tiles
 };
-
-// bits [c0, c0+64) of dgrid row u, built from the agent's tiles in LDS
-__device__ __forceinline__ void row_word(const State& s, const DjLds& L, int pad, int u, int w,
-                                         uint64_t& f, uint64_t& o) {
-  f = o = 0;
-  const int X = u - pad;
-  if (X < 0 || X >= s.Wp) return;
-  const int Y0 = 64 * w - pad;  // map column of bit 0
-  const int tj0 = Y0 < 0 ? 0 : (Y0 >> 3), tj1 = min((Y0 + 63) >> 3, s.TC - 1);
-  const int sh = (X & 7) * 8;
-  for (int tj = tj0; tj <= tj1; ++tj) {
-    const int t = (int)tile_index(s.TCS, X >> 3, tj);
-    const uint64_t fb = (L.tf[t] >> sh) & 0xFFull, obb = (L.to[t] >> sh) & 0xFFull;
-    const int off = 8 * tj - Y0;  // bit position of the tile's column 0
-    if (off >= 0) {
-      f |= fb << off;
-      o |= obb << off;
-    } else {
-      f |= fb >> -off;
-      o |= obb >> -off;
-    }
-  }
-}
 
 }  // namespace
 
@@ -102,7 +79,8 @@ __global__ __launch_bounds__(kDjThreads) void dijkstra_kernel(State s, int pad, 
   for (int i = tid; i < NW; i += kDjThreads) {
     const int u = i / RW, w = i - u * RW;
     uint64_t f, o;
-    row_word(s, L, pad, u, w, f, o);
+    f = row_word(s, L.tf, pad, u, w);
+    o = row_word(s, L.to, pad, u, w);
     const uint64_t in = (w == RW - 1) ? last : ~0ull;
     L.ob[i] = o & ~f & in;
     L.tg[i] = ~(f ^ o) & in;

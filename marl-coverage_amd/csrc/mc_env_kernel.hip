@@ -1001,8 +1001,19 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       const uint32_t fc = free_old + c->cnt_free;
       const uint32_t vc = vis_old + c->cnt_vis;
       const int cs = currstep0 + 1;                          // :154
-      double r = c->pen;                                     // :120,132-145
-      r += (double)c->cnt_vis;                               // :151,:256
+      // observe() :206-258 returns the float32 sum of the agents' distance
+      // terms (dist_reward, agent order) plus the union delta (float64)
+      float dsum = 0.0f;
+      if (s.dist) {
+        for (int i = 0; i < N; ++i) {
+          const int dx = L.x[i] - L.x0[i], dy = L.y[i] - L.y0[i];
+          const int k = dx == 1 ? 1 : (dy == 1 ? 2 : (dx == -1 ? 3 : (dy == -1 ? 4 : 0)));
+          const float* pr = s.dist_pre + ((size_t)e * N + i) * 8;
+          dsum = __fadd_rn(dsum, dist_value(pr[1 + k], pr[0]));  // :222-223,239-240
+        }
+      }
+      const double obs_reward = (double)dsum + (double)c->cnt_vis;
+      double r = c->pen + obs_reward;                        // :120,132-151
       const double pc = (double)fc / (double)numfree;        // :552
       double dt = dthresh0;
       const double thr = (1.0 < dt) ? 1.0 : dt;              // min(done_thresh, 1)

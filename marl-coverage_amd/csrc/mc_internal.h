@@ -62,6 +62,7 @@ struct State {
   int sensor, nbeams, sq_r;
   double pen, term, dincr;
   int maxsteps, comm_r, sst, auto_reset, grid_mode;
+  int dist;                // dist_reward: add the pre-sense distance terms
   uint64_t seed;
 
   const uint64_t* grid_neg;
@@ -84,6 +85,7 @@ struct State {
   uint32_t* episode;
   uint32_t* err;
   uint64_t* stamps;        // diagnostic builds (-DMC_STAMPS) only: [B][16] s_memtime
+  const float* dist_pre;   // dist_reward: [B][N][8] max(d), d of the 5 end cells (mc_dist.hip)
 };
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane

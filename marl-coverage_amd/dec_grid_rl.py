@@ -200,6 +200,9 @@ class DecGridRL:
         torch = self._torch
         obs = env.obs[0].to("cpu", non_blocking=False)
         self._obs_np = obs.numpy().astype(np.float64)
+        if env.dist_obs is not None and not self._dijkstra_input:
+            # float distance layer (the dijkstra path overwrites it, :354-358)
+            self._obs_np[:, 3] = env.dist_obs[0].cpu().numpy().astype(np.float64)
         pos = env.get_state(_lib.FIELD_POS)[0].cpu().numpy()
         self._xinds = pos[:, 0].astype(int)
         self._yinds = pos[:, 1].astype(int)

@@ -107,7 +107,4 @@ def check_against_golden(env):
     return check
 
 
-def needs_layers(case):
-    """Golden cases using the dist_reward layer / reward (not in the HIP path yet)."""
-    c = case["meta"]["config"]
-    return bool(c.get("dist_reward"))
+

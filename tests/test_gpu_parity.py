@@ -8,7 +8,7 @@ import zlib
 import numpy as np
 import pytest
 
-from golden_util import case_names, check_against_golden, load_case, make_env, needs_layers, replay
+from golden_util import case_names, check_against_golden, load_case, make_env, replay
 from gpu_util import compare_env, device_state, oracle_from_device, ref_action
 from oracle.cpu_ref import DecGridRLRef
 
@@ -42,8 +42,6 @@ def base_cfg(**kw):
 def test_facade_matches_reference_golden(torch_cuda, name):
     import marlcov
     case = load_case(name)
-    if needs_layers(case):
-        pytest.skip("dist_reward layer / reward is not in the HIP path yet (SURVEY 8f)")
     env = make_env(marlcov.DecGridRL, case)
     replay(env, case, check_against_golden(env))
 
@@ -51,6 +49,15 @@ def test_facade_matches_reference_golden(torch_cuda, name):
 # ---------------------------------------------------------------------------
 # 2. batched env vs one oracle env per batch entry, random actions
 # ---------------------------------------------------------------------------
+def full_obs(env, obs, cfg):
+    """uint8 obs as float64, with the float32 distance layer in place (the
+    reference's z[i][3] when dist_reward is on and dijkstra_input is off)."""
+    o = obs.cpu().numpy().astype(np.float64)
+    if env.dist_obs is not None and not cfg.get("dijkstra_input"):
+        o[:, :, 3] = env.dist_obs.cpu().numpy().astype(np.float64)
+    return o
+
+
 def bern(rs, w, l, p):
     return rs.choice([1.0, -1.0], size=(w, l), p=[1 - p, p])
 
@@ -103,6 +110,16 @@ BATCH_CASES = {
                           lambda rs: tri(rs, 36, 28), 8, 60),
     "dijkstra_c2_like": (base_cfg(numrobot=4, dijkstra_input=1), lambda rs: bern(rs, 128, 128, 0.1),
                          4, 12),
+    # dist_reward: float32 distance terms in the reward and
+    # the float obs layer; with dijkstra_input too the path overwrites it
+    "dist_lidar_n3": (base_cfg(numrobot=3, dist_reward=1, sensor_config={"num_lasers": 15, "range": 5}),
+                      lambda rs: bern(rs, 30, 26, 0.15), 6, 40),
+    "dist_square_ego3": (base_cfg(numrobot=2, dist_reward=1, egoradius=3, sensor_type="square_sensor",
+                                  sensor_config={"range": 2}), lambda rs: tri(rs, 22, 22), 6, 40),
+    "dist_and_dijkstra": (base_cfg(numrobot=2, dist_reward=1, dijkstra_input=1,
+                                   sensor_config={"num_lasers": 9, "range": 4}),
+                          lambda rs: bern(rs, 20, 20, 0.1), 6, 40),
+    "dist_c5_like_n16": (base_cfg(numrobot=16, dist_reward=1), lambda rs: bern(rs, 64, 64, 0.1), 2, 6),
 }
 
 
@@ -123,7 +140,7 @@ def test_batch_matches_oracle(torch_cuda, name):
     env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False, want_adjacency=True)
     obs, adj = env.reset(positions=np.stack(pos))
     st = device_state(env)
-    obs_h = obs.cpu().numpy()
+    obs_h = full_obs(env, obs, cfg)
     for b in range(B):
         compare_env(st, b, refs[b], f"{name} reset env {b}")
         np.testing.assert_array_equal(obs_h[b], refs[b].get_egocentric_observations(),
@@ -133,8 +150,8 @@ def test_batch_matches_oracle(torch_cuda, name):
         acts[rs.rand(B, N) < 0.08] = rs.choice([4, 7, 200])
         acts[rs.rand(B) < 0.05, 0] = 255
         (obs, adj), rew, done = env.step(torch.from_numpy(acts).to(env.device))
-        obs_h, rew_h, done_h, adj_h = (obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy(),
-                                       adj.cpu().numpy())
+        obs_h, rew_h, done_h, adj_h = (full_obs(env, obs, cfg), rew.cpu().numpy(),
+                                       done.cpu().numpy(), adj.cpu().numpy())
         st = device_state(env)
         for b in range(B):
             o, r, d = refs[b].step(ref_action(acts[b]))

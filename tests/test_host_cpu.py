@@ -63,8 +63,6 @@ def _cfg(**kw):
     (dict(num_agents=65), "numrobot"),
     (dict(num_agents=0), "numrobot"),
     (dict(width=2), "padded grid"),
-    (dict(dist_reward=1), "dist_reward"),
-    (dict(dist_reward=1, dijkstra_input=1), "dist_reward"),
     (dict(lidar_range=40.0), "range"),
     (dict(egoradius=40, pad=40), "egoradius"),
     (dict(num_agents=64, sensor_type=1, square_radius=20), "window tiles"),
