@@ -36,6 +36,10 @@ CONFIGS = {
                desc="C2: 4 agents, 128x128 grid p_obst=0.1, lidar 21 beams R=10, egoradius 2"),
     "c4": dict(numrobot=8, width=256, sensor_config={"num_lasers": 360, "range": 20}, envs=8192,
                desc="C4: 8 agents, 256x256 grid p_obst=0.1, lidar 360 beams R=20, egoradius 2"),
+    "c5": dict(numrobot=16, width=512, sensor_config={"num_lasers": 21, "range": 10}, envs=8192,
+               extra={"dist_reward": 1}, maxsteps=2000,
+               desc="C5: 16 agents, 512x512 grid p_obst=0.1, lidar 21 beams R=10, dist_reward "
+                    "(frontier-coverage reward, float32 distance layer)"),
     # C2 with the dijkstra_input obs layer (BSA/BA*-style
     # controllers); not a BASELINE metric config
     "c2_dijkstra": dict(numrobot=4, width=128, sensor_config={"num_lasers": 21, "range": 10}, envs=4096,
@@ -129,7 +133,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=8)
     ap.add_argument("--cpu-secs", type=float, default=2.5)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--maxsteps", type=int, default=1000, help="episode length (auto-reset on done)")
+    ap.add_argument("--maxsteps", type=int, default=None,
+                    help="episode length (auto-reset on done); default: the config's (1000, C5 2000)")
     ap.add_argument("--eager", action="store_true", help="plain launches + per-launch events (no hipGraph)")
     ap.add_argument("--graph-chunk", type=int, default=100, help="steps captured per hipGraph")
     args = ap.parse_args()
@@ -139,6 +144,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     c = CONFIGS[args.config]
     B = args.envs or c["envs"]
+    if args.maxsteps is None:
+        args.maxsteps = c.get("maxsteps", 1000)
 
     cpu = None
     if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu:
@@ -237,9 +244,13 @@ def main():
     n_gpus = world
     value = aggregate_rate(B, n_gpus, K, elapsed)
     dj = bool(cfg.get("dijkstra_input"))
+    dr = bool(cfg.get("dist_reward"))
+    # §8(d): C5's float32 distance layer is 4 B per cell (100 B per agent at
+    # E=5) and its two transforms read the whole bit map
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
-                                         layers=4 if dj else 3,
-                                         full_map_cells=(c["width"] + 2) ** 2 if dj else 0)
+                                         layers=3 + (4 if dr else 0) + (1 if dj else 0),
+                                         full_map_cells=(c["width"] + 2 + 2 * cfg["egoradius"]) ** 2
+                                         if (dj or dr) else 0)
     achieved = bpe * B / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
     line = {
