@@ -66,6 +66,7 @@ struct Env {
   size_t dt_lds = 0;  // dist_reward: LDS bytes of the distance kernel
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
+  bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
   void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
@@ -312,6 +313,11 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->dj_lds = need;
   }
   if (c.dist_reward) {
+    if (c.width + c.length + 4 * c.pad >= 65535) {
+      mc_destroy(E);
+      return fail(MC_EINVAL, "dist_reward: grid %dx%d too large for 16-bit distances", c.width,
+                  c.length);
+    }
     const size_t need = mc::dist_lds_bytes(s, c.pad);
     int maxlds = 0;
     if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
@@ -509,6 +515,7 @@ static int dist_terms(Env* E, int post, hipStream_t st) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dist_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dt_lds));
   HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, post, E->dist_pre, E->dist_obs, st));
+  E->dist_pre_stale = !post;  // a POST transform leaves PRE data for the next step
   return MC_OK;
 }
 
@@ -544,8 +551,10 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* 
   hipStream_t st = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(E->device));
   if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
-  rc = dist_terms(E, 0, st);  // observe() reads the maps before sensing
-  if (rc) return rc;
+  if (E->cfg.map_sharing || E->dist_pre_stale) {
+    rc = dist_terms(E, 0, st);  // observe() reads the maps before sensing
+    if (rc) return rc;
+  }
   HIP_TRY(mc::launch_env(E->s, mc::MODE_STEP, dev_actions, nullptr, nullptr, dev_reward, dev_done,
                          (uint8_t*)dev_obs, dev_adj, E->nt, launch_epw(E), st));
   rc = dijkstra_layer(E, dev_obs, st);
@@ -581,6 +590,7 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (f == MC_FIELD_GRID_NEG || f == MC_FIELD_GRID_POS || f == MC_FIELD_NUMFREE) E->grids_set = true;
+  E->dist_pre_stale = true;  // uploaded maps / positions: recompute the PRE terms
   return MC_OK;
 }
 

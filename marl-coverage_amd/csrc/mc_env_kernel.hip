@@ -626,7 +626,6 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 #else
       // marks of lower-index agents in this tile (bounded by N-1 so a
       // compile-time N unrolls it: the reads of all b are then in flight)
-#pragma unroll
       for (int b = 0; b < s.N - 1; ++b) {
         if (b >= a) break;
 #endif

@@ -120,6 +120,11 @@ BATCH_CASES = {
                                    sensor_config={"num_lasers": 9, "range": 4}),
                           lambda rs: bern(rs, 20, 20, 0.1), 6, 40),
     "dist_c5_like_n16": (base_cfg(numrobot=16, dist_reward=1), lambda rs: bern(rs, 64, 64, 0.1), 2, 6),
+    # map sharing changes the maps at the start of a step: the PRE transform
+    # runs again instead of reusing the previous step's POST data
+    "dist_map_sharing": (base_cfg(numrobot=4, dist_reward=1, comm_radius=6, allow_comm=1, map_sharing=1,
+                                  sensor_config={"num_lasers": 11, "range": 4}),
+                         lambda rs: bern(rs, 30, 30, 0.15), 6, 30),
 }
 
 
@@ -168,10 +173,11 @@ def test_batch_matches_oracle(torch_cuda, name):
 # 3. auto-reset: done envs restart in the same launch; the new episode equals
 #    the oracle's reset at the device-drawn start cells
 # ---------------------------------------------------------------------------
-def test_auto_reset_matches_oracle_reset(torch_cuda):
+@pytest.mark.parametrize("dist", [0, 1])
+def test_auto_reset_matches_oracle_reset(torch_cuda, dist):
     import marlcov
     torch = torch_cuda
-    cfg = base_cfg(numrobot=3, maxsteps=6, sensor_config={"num_lasers": 11, "range": 4})
+    cfg = base_cfg(numrobot=3, maxsteps=6, dist_reward=dist, sensor_config={"num_lasers": 11, "range": 4})
     rs = np.random.RandomState(7)
     B = 16
     grids = [bern(rs, 24, 24, 0.2) for _ in range(B)]
@@ -183,7 +189,7 @@ def test_auto_reset_matches_oracle_reset(torch_cuda):
     for t in range(20):
         acts = rs.randint(0, 4, size=(B, 3)).astype(np.uint8)
         obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
-        obs_h, rew_h, done_h = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
         st = device_state(env)
         for b in range(B):
             o, r, d = refs[b].step(ref_action(acts[b]))
@@ -246,7 +252,7 @@ def test_c2_full_size_invariants_and_sampled_parity(torch_cuda):
     for t in range(8):
         acts = rs.randint(0, 4, size=(B, 4)).astype(np.uint8)
         obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
-        obs_h, rew_h, done_h = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
         st = device_state(env)
         for b in sample:
             o, r, d = refs[b].step(acts[b].astype(np.int64))
