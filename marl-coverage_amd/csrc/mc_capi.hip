@@ -27,8 +27,11 @@ hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* 
                            hipStream_t stream);
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream);
+hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
+                            uint32_t* list, uint32_t* count, hipStream_t stream);
 size_t dist_lds_bytes(const State& s, int pad);
-__global__ void dist_kernel(State s, int pad, int post, float* pre_out, float* dist_obs);
+__global__ void dist_kernel(State s, int pad, int post, float* pre_out, float* dist_obs,
+                            const uint32_t* list, const uint32_t* count);
 size_t dijkstra_lds_bytes(const State& s, int pad);
 __global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
 }  // namespace mc
@@ -66,6 +69,7 @@ struct Env {
   size_t dt_lds = 0;  // dist_reward: LDS bytes of the distance kernel
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
+  uint32_t* dist_list = nullptr;  // dist_reward: [B*N] maps for the full transform + count
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
@@ -336,6 +340,18 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     }
     E->dist_pre = (float*)q;
     E->s.dist_pre = E->dist_pre;
+    // (M, witness) per map, M = -1 (unknown) until a full transform; the
+    // work list of the full transform and its count
+    void *mw = nullptr, *lq = nullptr;
+    if (dev_alloc(E, &mw, (size_t)s.B * s.N * 8) != MC_OK ||
+        dev_alloc(E, &lq, ((size_t)s.B * s.N + 1) * 4) != MC_OK ||
+        hipMemset(mw, 0xFF, (size_t)s.B * s.N * 8) != hipSuccess) {
+      std::string msg = g_err;
+      mc_destroy(E);
+      return fail(MC_EHIP, "dist_reward state: %s", msg.c_str());
+    }
+    E->s.dist_mw = (int32_t*)mw;
+    E->dist_list = (uint32_t*)lq;
   }
   mc_layout& L = E->lay;
   L.tile_rows = 4 * s.TRS;
@@ -514,7 +530,11 @@ static int dist_terms(Env* E, int post, hipStream_t st) {
   if (E->dt_lds > 65536)
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dist_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dt_lds));
-  HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, post, E->dist_pre, E->dist_obs, st));
+  if (post)  // window search per map, full transform for the maps whose max(d) may have changed
+    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 1,
+                                 E->dist_list, st));
+  else
+    HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, 0, E->dist_pre, E->dist_obs, st));
   E->dist_pre_stale = !post;  // a POST transform leaves PRE data for the next step
   return MC_OK;
 }
@@ -591,6 +611,8 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (f == MC_FIELD_GRID_NEG || f == MC_FIELD_GRID_POS || f == MC_FIELD_NUMFREE) E->grids_set = true;
   E->dist_pre_stale = true;  // uploaded maps / positions: recompute the PRE terms
+  if (E->s.dist_mw)  // and max(d) of every map
+    HIP_TRY(hipMemsetAsync(E->s.dist_mw, 0xFF, (size_t)E->s.B * E->s.N * 8, (hipStream_t)stream));
   return MC_OK;
 }
 

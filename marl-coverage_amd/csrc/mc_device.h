@@ -36,6 +36,39 @@ __device__ __forceinline__ float dist_value(float d, float M) {
   return M > 0.0f ? __fsub_rn(1.0f, __fdiv_rn(d, M)) : __fsub_rn(1.0f, d);
 }
 
+// dist_reward witness cell of a packed (x << 16) | (y & 0xFFFF) word (map
+// coordinates, signed 16-bit halves: the witness may lie in the pad ring)
+__device__ __forceinline__ int witness_x(int32_t w) { return w >> 16; }
+__device__ __forceinline__ int witness_y(int32_t w) { return (int)(int16_t)(w & 0xFFFF); }
+__device__ __forceinline__ int32_t pack_witness(int x, int y) {
+  return (int32_t)(((uint32_t)x << 16) | ((uint32_t)y & 0xFFFFu));
+}
+
+// true when a set bit of tile nb (cell (r, c) = map cell (x0 + r, y0 + c))
+// lies at L1 distance < M from map cell (wx, wy).  The tile's bounding box
+// rejects almost every tile; the exact row-by-row test runs only near the
+// witness.
+__device__ __forceinline__ bool bits_within(uint64_t nb, int x0, int y0, int wx, int wy, int M) {
+  const int bx = max(0, max(x0 - wx, wx - (x0 + 7)));
+  const int by = max(0, max(y0 - wy, wy - (y0 + 7)));
+  if (bx + by >= M) return false;
+  const int p = wy - y0;  // witness column relative to the tile
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)(nb >> (8 * r)) & 0xFFu;
+    if (!row) continue;
+    int dy;
+    if (p < 0) dy = __ffs(row) - 1 - p;
+    else if (p > 7) dy = p - (31 - __clz(row));
+    else {
+      const uint32_t lo = row & ((2u << p) - 1u), hi = row >> p;
+      dy = lo ? p - (31 - __clz(lo)) : 8;
+      if (hi) dy = min(dy, __ffs(hi) - 1);
+    }
+    if (abs(x0 + r - wx) + dy < M) return true;
+  }
+  return false;
+}
+
 // bit of cell (r, c) inside its 8x8 tile
 __device__ __forceinline__ int tile_bit(int r, int c) { return ((r & 7) << 3) | (c & 7); }
 

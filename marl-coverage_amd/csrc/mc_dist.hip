@@ -51,13 +51,22 @@ constexpr int kInf = 1 << 20;             // "no covered cell in this row"
 
 __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int post,
                                                           float* __restrict__ pre_out,
-                                                          float* __restrict__ dist_obs) {
+                                                          float* __restrict__ dist_obs,
+                                                          const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_d[kMaxTargets];
-  __shared__ int s_max, s_cov;
+  __shared__ int s_cov;
+  __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
   __shared__ int s_cpre[kChunks][kStrip], s_csuf[kChunks][kStrip];  // chunk minima per column
-  const int e = blockIdx.x / s.N, a = blockIdx.x - e * s.N;
   const int tid = threadIdx.x;
+  // every map (list == nullptr: one workgroup per (env, agent)), or the maps
+  // of a device work list (a fixed grid strides over *count entries: the
+  // count is uniform, so every wave reaches the end)
+  const uint32_t n_items = list ? *count : (uint32_t)gridDim.x;
+  for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
+  const uint32_t ea = list ? list[it] : it;
+  const int e = (int)(ea / (uint32_t)s.N), a = (int)(ea - (uint32_t)e * s.N);
   const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6, NW = RX * RW;
   // LDS: C row bitboard [RX][RW] u64 | NL, NR [RX][RW] i32 | G strip [RX][kStrip] u32
   uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
@@ -87,7 +96,7 @@ __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int 
 
   for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
   if (tid == 0) {
-    s_max = 0;
+    s_key = 0;
     s_cov = 0;
   }
   const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
@@ -129,7 +138,7 @@ __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int 
   const int col = tid % kStrip, chunk = tid / kStrip;
   const int clen = (RX + kChunks - 1) / kChunks;
   const int u0 = chunk * clen, u1 = min(RX, u0 + clen);
-  int vmax = 0;
+  int vmax = -1, ubest = 0, vbest = 0;  // this thread's first maximum
   for (int st = 0; cov && st < RW * (64 / kStrip); ++st) {
     const int w = st / (64 / kStrip), c0 = st * kStrip;  // word of the strip, first column
     // row pass: g(u, c0 + j) for the strip cells (u, j) = (i / kStrip, i % kStrip)
@@ -170,7 +179,11 @@ __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int 
       const uint32_t gw = G[u * kStrip + col];
       run = min(run, (int)(gw & 0xFFFFu) - u);
       const int d = min(u + run, (int)(gw >> 16) - u);
-      if (v < RY) vmax = max(vmax, d);
+      if (v < RY && d > vmax) {
+        vmax = d;
+        ubest = u;
+        vbest = v;
+      }
       G[u * kStrip + col] = (uint32_t)d;
     }
     __syncthreads();
@@ -182,12 +195,22 @@ __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int 
     }
     __syncthreads();
   }
-  if (cov) atomicMax(&s_max, vmax);
+  // witness: of the maxima, the one farthest from the robot (new coverage
+  // comes from around the robot, so it keeps M valid longest)
+  if (cov && vmax >= 0) {
+    const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
+    atomicMax(&s_key, ((unsigned long long)vmax << 40) | ((unsigned long long)far << 24) |
+                          ((unsigned long long)ubest << 12) | (unsigned long long)vbest);
+  }
   __syncthreads();
   // no covered cell: the restatement's convention (-1 everywhere); only the
   // discarded reset-time PRE term can see it
-  const int M = cov ? s_max : -1;
+  const int M = cov ? (int)(s_key >> 40) : -1;
   const float Mf = (float)M;
+  if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
+    const int wu = (int)((s_key >> 12) & 0xFFF), wv = (int)(s_key & 0xFFF);
+    reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
+  }
   if (post) {
     float* dst = dist_obs + ((size_t)e * s.N + a) * E * E;
     for (int t = 5 + tid; t < T; t += kDtThreads)
@@ -196,6 +219,8 @@ __global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int 
   float* pd = pre_out + ((size_t)e * s.N + a) * 8;
   if (tid == 0) pd[0] = Mf;
   if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
+  __syncthreads();  // the LDS is reused by the next item
+  }
 }
 
 size_t dist_lds_bytes(const State& s, int pad) {
@@ -208,7 +233,113 @@ size_t dist_lds_bytes(const State& s, int pad) {
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream) {
   hipLaunchKernelGGL(dist_kernel, dim3((unsigned)((size_t)s.B * s.N)), dim3(kDtThreads),
-                     dist_lds_bytes(s, pad), stream, s, pad, post, pre_out, dist_obs);
+                     dist_lds_bytes(s, pad), stream, s, pad, post, pre_out, dist_obs,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// POST terms without a full transform.  Sensing only adds covered cells, so
+// d only decreases and max(d) only decreases; the env kernel keeps M
+// (S.dist_mw) unless a new cell came closer than M to the witness, a cell
+// with d == M (then d(witness) is still M, and no cell exceeds M).  The
+// targets (the E x E crop and the 5 end cells of the next step) are near
+// the robot, so their d come from a bounded search: a 32 x 32 window
+// around the robot, dilated step by step as row bitboards (half a wave per
+// map, lane = window row).  d_in(t), the distance to the nearest covered
+// cell inside the window, is the true d(t) when d_in(t) <= the distance
+// b(t) from t to the nearest cell outside the window (any outside cell is
+// at least b(t) away; L1 paths inside a rectangle stay inside it).  A map
+// with an unknown M or a target the window cannot settle goes to the work
+// list of the full transform.
+// --------------------------------------------------------------------------
+constexpr int kLocalThreads = 256;
+constexpr int kWin = 32;
+
+__global__ __launch_bounds__(kLocalThreads) void dist_local_kernel(State s, int pad,
+                                                                   float* __restrict__ pre_out,
+                                                                   float* __restrict__ dist_obs,
+                                                                   uint32_t* __restrict__ list,
+                                                                   uint32_t* __restrict__ count) {
+  const int tid = threadIdx.x;
+  const uint32_t ea = (blockIdx.x * kLocalThreads + tid) / kWin;
+  const int r = tid & (kWin - 1);  // window row of this lane
+  const int hb = (tid & 63) & ~(kWin - 1);  // first lane of this half wave
+  if (ea >= (uint32_t)s.B * s.N) return;  // whole half waves
+  const int2 mw = reinterpret_cast<const int2*>(s.dist_mw)[ea];
+  const int M = mw.x;
+  const int E = s.E, T = 5 + E * E;
+  if (M < 0 || T > kWin) {
+    if (r == 0) list[atomicAdd(count, 1u)] = ea;
+    return;
+  }
+  const int2 p = reinterpret_cast<const int2*>(s.pos)[ea];
+  const int ti0 = (p.x - 12) >> 3, tj0 = (p.y - 12) >> 3;  // floor: window tile origin
+  const int X0 = 8 * ti0, Y0 = 8 * tj0;
+  // row r of the window: bits of tiles (ti0 + r/8, tj0 .. tj0 + 3)
+  uint32_t cur = 0;
+  {
+    const int ti = ti0 + (r >> 3);
+    const uint64_t* ft = s.freem + (size_t)ea * s.MT;
+    if (ti >= 0 && ti < s.TR) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int tj = tj0 + q;
+        if (tj >= 0 && tj < s.TC)
+          cur |= (uint32_t)((ft[tile_index(s.TCS, ti, tj)] >> (8 * (r & 7))) & 0xFFull) << (8 * q);
+      }
+    }
+  }
+  // target of this lane (map coordinates), window-local (tr, tc), bound b
+  int tx, ty;
+  if (r < 5) {  // distance_map[x, y] of the next step's end cells (quirk: no pad offset)
+    tx = p.x + (r == 1 ? 1 : (r == 3 ? -1 : 0)) - pad;
+    ty = p.y + (r == 2 ? 1 : (r == 4 ? -1 : 0)) - pad;
+  } else {
+    const int k = r < T ? r - 5 : 0, rr = k / E;
+    tx = p.x - s.ego + rr;
+    ty = p.y - s.ego + (k - rr * E);
+  }
+  const int tr = tx - X0, tc = ty - Y0;
+  const bool live = r < T;
+  const bool inwin = tr >= 0 && tr < kWin && tc >= 0 && tc < kWin;
+  const int b = inwin ? min(min(tr, kWin - 1 - tr), min(tc, kWin - 1 - tc)) + 1 : 0;
+  int dt = -1;
+  for (int k = 0; k < kWin / 2; ++k) {
+    const uint32_t row = (uint32_t)__shfl((int)cur, hb + (inwin ? tr : 0), 64);
+    if (live && inwin && dt < 0 && ((row >> tc) & 1u)) dt = k;
+    const uint64_t pend = __ballot(live && inwin && dt < 0 && k < b);
+    if (((pend >> hb) & 0xFFFFFFFFull) == 0) break;
+    const uint32_t up = (uint32_t)__shfl((int)cur, hb + (r > 0 ? r - 1 : 0), 64);
+    const uint32_t dn = (uint32_t)__shfl((int)cur, hb + (r < kWin - 1 ? r + 1 : r), 64);
+    cur |= (cur << 1) | (cur >> 1) | (r > 0 ? up : 0u) | (r < kWin - 1 ? dn : 0u);
+  }
+  const bool ok = !live || (inwin && dt >= 0 && dt <= b);
+  const uint64_t bad = __ballot(!ok);
+  if ((bad >> hb) & 0xFFFFFFFFull) {
+    if (r == 0) list[atomicAdd(count, 1u)] = ea;
+    return;
+  }
+  float* pd = pre_out + (size_t)ea * 8;
+  if (r == 0) pd[0] = (float)M;
+  if (r < 5) pd[1 + r] = (float)dt;
+  else if (live) dist_obs[(size_t)ea * E * E + (r - 5)] = dist_value((float)dt, (float)M);
+}
+
+// POST: the window search for every map, then the full transform for the
+// maps it listed.  The list grid is fixed (hipGraph capture) and strides.
+hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
+                            uint32_t* list, uint32_t* count, hipStream_t stream) {
+  const size_t maps = (size_t)s.B * s.N;
+  hipError_t err = hipMemsetAsync(count, 0, 4, stream);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(dist_local_kernel, dim3((unsigned)((maps * kWin + kLocalThreads - 1) / kLocalThreads)),
+                     dim3(kLocalThreads), 0, stream, s, pad, pre_out, dist_obs, list, count);
+  err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
+  hipLaunchKernelGGL(dist_kernel, dim3(grid), dim3(kDtThreads), dist_lds_bytes(s, pad), stream, s,
+                     pad, 1, pre_out, dist_obs, (const uint32_t*)list, (const uint32_t*)count);
   return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ struct Scal {
   uint32_t ep;
   int32_t do_reset;
   int32_t pad_;
+  uint64_t dist_hit;   // dist_reward: agents whose witness cell got closer than M
 };
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 
@@ -81,6 +82,7 @@ struct Lds {
   Beam* beams;
   int32_t *x0, *y0, *x, *y;  // pre-move / post-move cells
   int32_t *bx, *by;          // tile-block origin (tile units) of each agent
+  int32_t *dm, *dw;          // dist_reward: M and witness of each agent's free map
   Scal* sc;
   uint8_t* act;
   WT* sink;                  // [64] target of lidar marks a lane does not make
@@ -111,7 +113,9 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   L.y = L.x + s.N;
   L.bx = L.y + s.N;
   L.by = L.bx + s.N;
-  q += (((size_t)s.N * 6 * 4) + 15) & ~(size_t)15;
+  L.dm = L.by + s.N;
+  L.dw = L.dm + s.N;
+  q += (((size_t)s.N * 8 * 4) + 15) & ~(size_t)15;
   L.sc = reinterpret_cast<Scal*>(q);
   q += 64;
   L.act = reinterpret_cast<uint8_t*>(q);
@@ -643,6 +647,13 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       }
       I.nu[k] = cand;
       cv += __popcll(cand);
+      // dist_reward: a new free cell closer than M to the agent's witness
+      // may lower max(d): the map's M must be recomputed (mc_dist.hip)
+      if (s.dist && I.nf[k]) {
+        const int M = L.dm[a], w = L.dw[a];
+        if (M > 0 && bits_within(I.nf[k], 8 * gi, 8 * gj, witness_x(w), witness_y(w), M))
+          atomicOr((unsigned long long*)&L.sc->dist_hit, 1ull << a);
+      }
     }
   }
   if (cf) atomicAdd(&L.sc->cnt_free, cf);
@@ -968,6 +979,12 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     L.sc->cnt_free = 0;
     L.sc->cnt_vis = 0;
     L.sc->do_reset = 0;
+    L.sc->dist_hit = 0;
+  }
+  if (s.dist && C.sub < N) {  // dist_reward: M and witness of each free map
+    const int2 mw = reinterpret_cast<const int2*>(s.dist_mw)[(size_t)e * N + C.sub];
+    L.dm[C.sub] = mw.x;
+    L.dw[C.sub] = mw.y;
   }
   if (lidar) {
     if (C.sub < s.nbeams) reinterpret_cast<int4*>(L.beams)[C.sub] = bm0;
@@ -1056,6 +1073,11 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     if (C.sub < N)
       reinterpret_cast<int2*>(s.pos)[(size_t)e * N + C.sub] = make_int2(L.x[C.sub], L.y[C.sub]);
     if (C.sub == 0) s.moved[e] = L.sc->moved;
+    // dist_reward: a reset map, or one whose witness got closer than M,
+    // has an unknown M now (recomputed by the full transform, mc_dist.hip)
+    if (s.dist && C.sub < N &&
+        (reset_req || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
+      s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
   }
   STAMP(8);
 #if !(defined(MC_ABL) && MC_ABL == 5)

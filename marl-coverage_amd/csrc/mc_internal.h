@@ -86,6 +86,12 @@ struct State {
   uint32_t* err;
   uint64_t* stamps;        // diagnostic builds (-DMC_STAMPS) only: [B][16] s_memtime
   const float* dist_pre;   // dist_reward: [B][N][8] max(d), d of the 5 end cells (mc_dist.hip)
+  // dist_reward: [B][N] (M, witness) of each free map: M = max(d) over the
+  // extended grid (-1: unknown), witness = a cell with d == M (map
+  // coordinates, (x << 16) | (y & 0xFFFF), signed halves).  The env kernel
+  // sets M = -1 when sensing covers a cell closer than M to the witness (or
+  // the env resets); otherwise M is unchanged (mc_dist.hip).
+  int32_t* dist_mw;
 };
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
@@ -120,7 +126,7 @@ __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int r
   size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
   b += (((size_t)3 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / fp / op rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
-  b += (((size_t)N * 6 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by
+  b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
   b += 64;                                             // scalars
   b += ((size_t)N + 15) & ~(size_t)15;                 // actions
   b += 64 * (size_t)rowbytes;                          // per-lane sink words (lidar marks)
@@ -171,6 +177,7 @@ __device__ __forceinline__ void specialize(State& s) {
     s.mg_LcE = magic_div(3 * (2 * SH::EGO + 1));
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
+  if constexpr (SH::EGO > 0) s.dist = 0;  // EGO matches only Lc == 3: no dist layer
 }
 
 }  // namespace mc

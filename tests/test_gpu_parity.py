@@ -120,6 +120,14 @@ BATCH_CASES = {
                                    sensor_config={"num_lasers": 9, "range": 4}),
                           lambda rs: bern(rs, 20, 20, 0.1), 6, 40),
     "dist_c5_like_n16": (base_cfg(numrobot=16, dist_reward=1), lambda rs: bern(rs, 64, 64, 0.1), 2, 6),
+    # long episodes: max(d) drops many times (the env kernel's witness test
+    # sends those maps to the full transform, the rest keep M and take their
+    # targets from the window search); single_square_tool keeps coverage thin
+    # and max(d) large
+    "dist_long_walk": (base_cfg(numrobot=4, dist_reward=1, sensor_config={"num_lasers": 9, "range": 3}),
+                       lambda rs: bern(rs, 40, 40, 0.1), 6, 150),
+    "dist_single_tool": (base_cfg(numrobot=3, dist_reward=1, single_square_tool=1, sensor_type="square_sensor",
+                                  sensor_config={"range": 1}), lambda rs: bern(rs, 36, 44, 0.1), 4, 120),
     # map sharing changes the maps at the start of a step: the PRE transform
     # runs again instead of reusing the previous step's POST data
     "dist_map_sharing": (base_cfg(numrobot=4, dist_reward=1, comm_radius=6, allow_comm=1, map_sharing=1,
@@ -262,6 +270,40 @@ def test_c2_full_size_invariants_and_sampled_parity(torch_cuda):
                 o, _ = refs[b].reset(False, None, positions=[tuple(x) for x in q])
             np.testing.assert_array_equal(obs_h[b], o)
             compare_env(st, b, refs[b], f"c2 t={t} env {b}")
+
+
+def test_c5_dist_sampled_parity(torch_cuda):
+    """BASELINE configs[4] shape (16 agents, 512x512, dist_reward) on 256 envs:
+    after 40 steps of incremental max(d) tracking, envs re-built in the oracle
+    from the device maps (fresh distance transforms) step on bit-exactly."""
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=2000)
+    B = 256
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
+                                   seed=5, auto_reset=True)
+    env.reset()
+    g = torch.Generator(device=env.device)
+    g.manual_seed(0)
+    for t in range(40):
+        acts = torch.randint(0, 4, (B, 16), dtype=torch.uint8, device=env.device, generator=g)
+        env.step(acts)
+    torch.cuda.synchronize()
+    env.check()
+    st = device_state(env)
+    sample = [3, 101, 200]
+    refs = {b: oracle_from_device(st, b, cfg) for b in sample}
+    rs = np.random.RandomState(12)
+    for t in range(4):
+        acts = rs.randint(0, 4, size=(B, 16)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h = full_obs(env, obs, cfg), rew.cpu().numpy()
+        st = device_state(env)
+        for b in sample:
+            o, r, d = refs[b].step(acts[b].astype(np.int64))
+            assert float(r) == rew_h[b], (t, b, float(r), rew_h[b])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=f"c5 t={t} env {b}")
+            compare_env(st, b, refs[b], f"c5 t={t} env {b}")
 
 
 def test_determinism_same_seed(torch_cuda):
