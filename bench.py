@@ -164,6 +164,8 @@ def main():
 
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
                maxsteps=args.maxsteps, **c.get("extra", {}))
+    dj = bool(cfg.get("dijkstra_input"))
+    dr = bool(cfg.get("dist_reward"))
     N = c["numrobot"]
     seeds = rank_seeds(rank)
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
@@ -234,6 +236,9 @@ def main():
         # duration from above (rocprofv3 in profiles/ gives the bare kernel)
         kern_ms = ev0.elapsed_time(ev1) / K
     env.check()
+    listed = None
+    if dr:  # maps the last step sent to the full distance transform (diagnostic)
+        listed = int(env.get_state(marlcov._lib.FIELD_DIST_LISTED).item())
 
     # scalar episode-return statistics: the only collective (outside timing)
     reward_sum += env.reward
@@ -243,8 +248,6 @@ def main():
 
     n_gpus = world
     value = aggregate_rate(B, n_gpus, K, elapsed)
-    dj = bool(cfg.get("dijkstra_input"))
-    dr = bool(cfg.get("dist_reward"))
     # §8(d): C5's float32 distance layer is 4 B per cell (100 B per agent at
     # E=5) and its two transforms read the whole bit map
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
@@ -268,7 +271,8 @@ def main():
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
                    "launch": "eager" if args.eager else "hipGraph replay",
-                   "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps},
+                   "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
+                   **({"dist_full_transforms_last_step": listed} if dr else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),

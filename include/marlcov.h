@@ -120,7 +120,14 @@ enum {
   MC_FIELD_NUMFREE = 11,     /* int32  [G]  count_nonzero(grid > 0) per grid   */
   MC_FIELD_GRID_NEG = 12,    /* uint64 [G][map] grid < 0                       */
   MC_FIELD_GRID_POS = 13,    /* uint64 [G][map] grid > 0                       */
-  MC_FIELD_COUNT = 14
+  /* dist_reward configs only (MC_EINVAL otherwise):                           */
+  MC_FIELD_DIST_MW = 14,     /* int32 [B][N][2] (M, witness): M = max of the map's
+                                L1 distance transform (-1 = unknown: the next
+                                POST runs the full transform), witness = a cell
+                                with d == M, (x << 16) | (y & 0xFFFF), map coords */
+  MC_FIELD_DIST_LISTED = 15, /* uint32 [1] maps the last POST sent to the full
+                                transform (read-only diagnostic)               */
+  MC_FIELD_COUNT = 16
 };
 
 int32_t mc_abi_version(void);

@@ -102,6 +102,8 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_NUMFREE: return {(void*)s.numfree, G * 4};
     case MC_FIELD_GRID_NEG: return {(void*)s.grid_neg, G * mw * 8};
     case MC_FIELD_GRID_POS: return {(void*)s.grid_pos, G * mw * 8};
+    case MC_FIELD_DIST_MW: return {s.dist_mw, s.dist_mw ? B * N * 8 : -1};
+    case MC_FIELD_DIST_LISTED: return {E->dist_list, E->dist_list ? 4 : -1};
     default: return {nullptr, -1};
   }
 }
@@ -606,6 +608,8 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   if (!E || !dev_src) return fail(MC_EINVAL, "mc_set_state: null argument");
   FieldDesc d = field(E, f);
   if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
+  if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED)
+    return fail(MC_EINVAL, "field %d is derived state (read-only)", f);
   if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));

@@ -174,7 +174,30 @@ def test_batch_matches_oracle(torch_cuda, name):
             np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
             np.testing.assert_array_equal(adj_h[b], refs[b]._adjacency_matrix, err_msg=tag + " adj")
             compare_env(st, b, refs[b], tag)
+        if cfg.get("dist_reward"):
+            check_dist_mw(env, refs, f"{name} t={t}")
     env.check()
+
+
+def check_dist_mw(env, refs, tag):
+    """Every known (M, witness) of the device equals the oracle's fresh
+    distance transform: M = its max, d(witness) = M."""
+    from marlcov import _lib
+    from oracle.cpu_ref import l1_distance_to_covered
+    mw = env.get_state(_lib.FIELD_DIST_MW).cpu().numpy()
+    known = 0
+    for b, ref in enumerate(refs):
+        p = ref._pad
+        for i in range(ref._numrobot):
+            M, w = int(mw[b, i, 0]), int(mw[b, i, 1])
+            if M < 0:
+                continue
+            known += 1
+            d = l1_distance_to_covered(ref._free_pad[i])
+            wx, wy = w >> 16, ((w & 0xFFFF) ^ 0x8000) - 0x8000
+            assert M == int(d.max()), (tag, b, i, M, d.max())
+            assert int(d[wx + p, wy + p]) == M, (tag, b, i, "witness", wx, wy)
+    assert known > 0, tag
 
 
 # ---------------------------------------------------------------------------
