@@ -30,8 +30,7 @@ hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float*
 hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
                             uint32_t* list, uint32_t* count, hipStream_t stream);
 size_t dist_lds_bytes(const State& s, int pad);
-__global__ void dist_kernel(State s, int pad, int post, float* pre_out, float* dist_obs,
-                            const uint32_t* list, const uint32_t* count);
+int dist_max_rows();
 size_t dijkstra_lds_bytes(const State& s, int pad);
 __global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
 }  // namespace mc
@@ -324,6 +323,11 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       return fail(MC_EINVAL, "dist_reward: grid %dx%d too large for 16-bit distances", c.width,
                   c.length);
     }
+    if (s.Wp + 2 * c.pad > mc::dist_max_rows()) {
+      mc_destroy(E);
+      return fail(MC_EINVAL, "dist_reward: %d extended rows exceed the transform's %d", s.Wp + 2 * c.pad,
+                  mc::dist_max_rows());
+    }
     const size_t need = mc::dist_lds_bytes(s, c.pad);
     int maxlds = 0;
     if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
@@ -529,9 +533,6 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
 // the env kernel's reward) or the obs layer of the maps after it (POST)
 static int dist_terms(Env* E, int post, hipStream_t st) {
   if (!E->cfg.dist_reward) return MC_OK;
-  if (E->dt_lds > 65536)
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dist_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dt_lds));
   if (post)  // window search per map, full transform for the maps whose max(d) may have changed
     HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 1,
                                  E->dist_list, st));

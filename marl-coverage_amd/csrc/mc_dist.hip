@@ -19,21 +19,26 @@
 //   g(u, v) = distance along row u to its nearest covered cell,
 //   d(u, v) = min over u' of |u - u'| + g(u', v)
 //           = min( u + min_{u'<=u} (g(u',v) - u'),  -u + min_{u'>=u} (g(u',v) + u') ),
-// a prefix-min and a suffix-min down every column.  One workgroup per
-// (env, agent) walks the extended grid in strips of 32 columns (half a word
-// of the LDS row bitboard): the row pass fills a [rows][32] strip of g in
-// LDS, the column pass runs the two scans as 8 row chunks per column (a
-// chunked parallel scan), and keeps max(d) and the d of the target cells.
-// Work is O(cells) per transform, independent of how far the maps are from
-// covered (a BFS by layers was O(cells * max d): 6 s per C5 step).
+// a prefix-min and a suffix-min down every column.  One workgroup per map
+// walks the extended grid in strips of 32 columns:
+//   row pass    a thread per row computes the strip's 32 g in registers (two
+//               bit scans with the nearest covered column left / right of the
+//               strip carried in registers) and writes them as u16 to LDS;
+//   column pass a thread per (column, chunk of kCL rows) loads its g into
+//               registers, publishes the chunk's minima of g - u and g + u,
+//               and after one barrier finishes both scans in registers
+//               (chunked parallel scan: no LDS latency inside the scans).
+// Work is O(cells) per transform; LDS holds the row bitboard and one u16
+// strip (~78 KB at C5: two workgroups per CU).
 //
 // PRE data: for the five cells the robot can end the next step on (stay, +x,
 //      +y, -x, -y), at the quirk index: pre[e][a][0] = max(d),
 //      pre[e][a][1 + k] = d of candidate k.  Every transform writes it.
-// POST (after the env kernel) also writes the E x E crop: the float32 obs
-//      layer.  Its PRE data serve the next step, whose sensing starts from
-//      these same maps; only map sharing (which changes them at the start of
-//      a step) or a state upload makes mc_step run a PRE transform first.
+// POST also writes the E x E crop: the float32 obs layer.  Its PRE data serve
+//      the next step, whose sensing starts from these same maps; only map
+//      sharing (which changes them at the start of a step) or a state upload
+//      makes mc_step run a PRE transform first.
+// Every transform also leaves (M, witness) for the incremental path below.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,199 +48,275 @@ namespace mc {
 
 namespace {
 constexpr int kDtThreads = 512;
-constexpr int kStrip = 32;                // columns per strip
-constexpr int kChunks = kDtThreads / kStrip;  // row chunks per column in the column pass
-constexpr int kMaxTargets = 32 * 32;
-constexpr int kInf = 1 << 20;             // "no covered cell in this row"
+constexpr int kStrip = 32;                     // columns per strip
+constexpr int kChunks = kDtThreads / kStrip;   // row chunks per column in the column pass
+constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
+constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
 }  // namespace
 
-__global__ __launch_bounds__(kDtThreads) void dist_kernel(State s, int pad, int post,
-                                                          float* __restrict__ pre_out,
-                                                          float* __restrict__ dist_obs,
-                                                          const uint32_t* __restrict__ list,
-                                                          const uint32_t* __restrict__ count) {
+// rows per column chunk: the instantiation (16, 33 or 52) whose kChunks
+// chunks cover RX; the strip holds kChunks * chunk rows (rows >= RX are
+// padding with no covered cell)
+__host__ __device__ constexpr int chunk_rows(int RX) { return RX <= 256 ? 16 : (RX <= 528 ? 33 : 52); }
+
+// LDS carve of the full transform (bytes): row bitboard | strip (u16, also the
+// tile staging area) | chunk minima | targets
+struct DtLds {
+  size_t cb, strip, mins, tgt, total;
+};
+__host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
+  DtLds L;
+  const int RW = (RY + 63) >> 6;
+  L.cb = (size_t)RX * RW * 8;
+  const size_t st = (size_t)kChunks * chunk_rows(RX) * kStrip * 2, tiles = (size_t)MT * 8;
+  L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
+  L.mins = (size_t)2 * kChunks * kStrip * 4;
+  L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
+  L.total = L.cb + L.strip + L.mins + L.tgt;
+  return L;
+}
+
+template <int kCL>
+__global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
+                                                            float* __restrict__ pre_out,
+                                                            float* __restrict__ dist_obs,
+                                                            const uint32_t* __restrict__ list,
+                                                            const uint32_t* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int s_d[kMaxTargets];
   __shared__ int s_cov;
   __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
-  __shared__ int s_cpre[kChunks][kStrip], s_csuf[kChunks][kStrip];  // chunk minima per column
   const int tid = threadIdx.x;
+  const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6;
+  const int E = s.E;
+  const int T = post ? 5 + E * E : 5;
+  const DtLds LL = dt_lds(RX, RY, s.MT, 5 + E * E);
+  uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
+  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kStrip]
+  constexpr int RXP = kChunks * kCL;                         // strip rows incl. padding
+  int* s_cpre = reinterpret_cast<int*>(smem + LL.cb + LL.strip);  // [kChunks][kStrip]
+  int* s_csuf = s_cpre + kChunks * kStrip;
+  int* s_d = reinterpret_cast<int*>(smem + LL.cb + LL.strip + LL.mins);
+  const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
   // of a device work list (a fixed grid strides over *count entries: the
   // count is uniform, so every wave reaches the end)
   const uint32_t n_items = list ? *count : (uint32_t)gridDim.x;
   for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
-  const uint32_t ea = list ? list[it] : it;
-  const int e = (int)(ea / (uint32_t)s.N), a = (int)(ea - (uint32_t)e * s.N);
-  const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6, NW = RX * RW;
-  // LDS: C row bitboard [RX][RW] u64 | NL, NR [RX][RW] i32 | G strip [RX][kStrip] u32
-  uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
-  int* NL = reinterpret_cast<int*>(Cb + NW);  // last covered column < 64w (or -kInf)
-  int* NR = NL + NW;                          // first covered column >= 64(w+1) (or kInf)
-  const uint64_t* free_t = s.freem + ((size_t)e * s.N + a) * s.MT;
-  const int px = s.pos[((size_t)e * s.N + a) * 2], py = s.pos[((size_t)e * s.N + a) * 2 + 1];
-  const int E = s.E;
-  // targets: [0, 5) the end cells of the next step (PRE data: the maps do
-  // not change between this transform and the next step's sensing unless
-  // map sharing runs first), [5, 5 + E*E) the crop (POST only)
-  const int T = post ? 5 + E * E : 5;
+    const uint32_t ea = list ? list[it] : it;
+    const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
+    const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
+    const int px = pp.x, py = pp.y;
 
-  // target t -> extended cell (u, v)
-  auto target = [&](int t, int& u, int& v) {
-    if (t >= 5) {
-      const int r = (t - 5) / E, c = (t - 5) - r * E;
-      u = px + pad - s.ego + r;
-      v = py + pad - s.ego + c;
-    } else {  // distance_map[x, y]: the padded-grid coordinates used as is
-      const int dx = t == 1 ? 1 : (t == 3 ? -1 : 0);
-      const int dy = t == 2 ? 1 : (t == 4 ? -1 : 0);
-      u = px + dx;
-      v = py + dy;
-    }
-  };
-
-  for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
-  if (tid == 0) {
-    s_key = 0;
-    s_cov = 0;
-  }
-  const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
-  {
-    // the agent's tiles into LDS first (coalesced, all loads in flight; the
-    // strip area is free until the strips start), then the row bitboard
-    uint64_t* tl = reinterpret_cast<uint64_t*>(NL + 2 * NW);
-#pragma unroll 4
-    for (int i = tid; i < s.MT; i += kDtThreads) tl[i] = free_t[i];
-    __syncthreads();
-    for (int i = tid; i < NW; i += kDtThreads) {
-      const int u = i / RW, w = i - u * RW;
-      Cb[i] = row_word(s, tl, pad, u, w) & ((w == RW - 1) ? last : ~0ull);
-    }
-  }
-  __syncthreads();
-  // nearest covered column outside each word, per row (one thread per row)
-  for (int u = tid; u < RX; u += kDtThreads) {
-    int l = -kInf;
-    for (int w = 0; w < RW; ++w) {
-      NL[u * RW + w] = l;
-      const uint64_t c = Cb[u * RW + w];
-      if (c) l = 64 * w + 63 - __clzll((long long)c);
-    }
-    int r = kInf;
-    for (int w = RW - 1; w >= 0; --w) {
-      NR[u * RW + w] = r;
-      const uint64_t c = Cb[u * RW + w];
-      if (c) r = 64 * w + __ffsll((unsigned long long)c) - 1;
-    }
-    if (l != -kInf) atomicOr(&s_cov, 1);
-  }
-  __syncthreads();
-  const bool cov = s_cov != 0;
-
-  // the strips.  G[u][b] packs g (low 16 bits, 0xFFFF = no covered cell in
-  // the row) and then the suffix minimum min_{u'>=u} (g(u') + u') (high 16).
-  uint32_t* G = reinterpret_cast<uint32_t*>(NR + NW);
-  const int col = tid % kStrip, chunk = tid / kStrip;
-  const int clen = (RX + kChunks - 1) / kChunks;
-  const int u0 = chunk * clen, u1 = min(RX, u0 + clen);
-  int vmax = -1, ubest = 0, vbest = 0;  // this thread's first maximum
-  for (int st = 0; cov && st < RW * (64 / kStrip); ++st) {
-    const int w = st / (64 / kStrip), c0 = st * kStrip;  // word of the strip, first column
-    // row pass: g(u, c0 + j) for the strip cells (u, j) = (i / kStrip, i % kStrip)
-    for (int i = tid; i < RX * kStrip; i += kDtThreads) {
-      const int u = i / kStrip, b = c0 + i % kStrip - 64 * w;  // bit in word w
-      const uint64_t c = Cb[u * RW + w];
-      const uint64_t le = c & low_mask(b + 1);  // covered at or left of b in the word
-      const uint64_t ge = c & ~low_mask(b);     // covered at or right of b
-      const int v = 64 * w + b;
-      const int left = le ? 64 * w + 63 - __clzll((long long)le) : NL[u * RW + w];
-      const int right = ge ? 64 * w + __ffsll((unsigned long long)ge) - 1 : NR[u * RW + w];
-      G[i] = (uint32_t)min(min(v - left, right - v), 0xFFFF);
-    }
-    __syncthreads();
-    // column pass: chunk-local minima of g - u and g + u
-    int pmin = kInf, smin = kInf;
-#pragma unroll 8
-    for (int u = u0; u < u1; ++u) {
-      const int gv = (int)(G[u * kStrip + col] & 0xFFFFu);
-      pmin = min(pmin, gv - u);
-      smin = min(smin, gv + u);
-    }
-    s_cpre[chunk][col] = pmin;
-    s_csuf[chunk][col] = smin;
-    __syncthreads();
-    int pin = kInf, sin_ = kInf;  // minima over the chunks before / after this one
-    for (int q = 0; q < chunk; ++q) pin = min(pin, s_cpre[q][col]);
-    for (int q = chunk + 1; q < kChunks; ++q) sin_ = min(sin_, s_csuf[q][col]);
-    int run = sin_;  // backward sweep: suffix minima into the high half
-    for (int u = u1 - 1; u >= u0; --u) {
-      const uint32_t gw = G[u * kStrip + col];
-      run = min(run, (int)(gw & 0xFFFFu) + u);
-      G[u * kStrip + col] = (gw & 0xFFFFu) | ((uint32_t)min(run, 0xFFFF) << 16);
-    }
-    const int v = c0 + col;
-    run = pin;  // forward sweep: d = min(u + prefix, suffix - u), kept in G
-    for (int u = u0; u < u1; ++u) {
-      const uint32_t gw = G[u * kStrip + col];
-      run = min(run, (int)(gw & 0xFFFFu) - u);
-      const int d = min(u + run, (int)(gw >> 16) - u);
-      if (v < RY && d > vmax) {
-        vmax = d;
-        ubest = u;
-        vbest = v;
+    // target t -> extended cell (u, v): [0, 5) the end cells of the next step
+    // (quirk: distance_map[x, y] with the padded-grid (x, y), no pad offset),
+    // [5, 5 + E*E) the crop (POST only)
+    auto target = [&](int t, int& u, int& v) {
+      if (t >= 5) {
+        const int r = (t - 5) / E, c = (t - 5) - r * E;
+        u = px + pad - s.ego + r;
+        v = py + pad - s.ego + c;
+      } else {
+        u = px + (t == 1 ? 1 : (t == 3 ? -1 : 0));
+        v = py + (t == 2 ? 1 : (t == 4 ? -1 : 0));
       }
-      G[u * kStrip + col] = (uint32_t)d;
+    };
+    for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
+    if (tid == 0) {
+      s_key = 0;
+      s_cov = 0;
+    }
+    {
+      // the agent's tiles into LDS first (coalesced, all loads in flight; the
+      // strip area is free until the strips start), then the row bitboard
+      uint64_t* tl = reinterpret_cast<uint64_t*>(G);
+#pragma unroll 4
+      for (int i = tid; i < s.MT; i += kDtThreads) tl[i] = free_t[i];
+      __syncthreads();
+      int any = 0;
+      for (int i = tid; i < RX * RW; i += kDtThreads) {
+        const int u = i / RW, w = i - u * RW;
+        const uint64_t c = row_word(s, tl, pad, u, w) & ((w == RW - 1) ? last : ~0ull);
+        Cb[i] = c;
+        any |= c != 0;
+      }
+      if (any) s_cov = 1;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += kDtThreads) {
-      int tu, tv;
-      target(t, tu, tv);
-      if (tu >= 0 && tu < RX && tv >= c0 && tv < c0 + kStrip && tv < RY)
-        s_d[t] = (int)G[tu * kStrip + (tv - c0)];
+    const bool cov = s_cov != 0;
+
+    // row-pass registers: a thread owns rows tid and tid + kDtThreads
+    int lastL[2] = {-kInf, -kInf};  // last covered column left of the strip
+    int nrw[2] = {-1, -1};          // next non-empty word after the current one (-1: not scanned)
+    const int col = tid % kStrip, chunk = tid / kStrip;
+    const int u0c = chunk * kCL;
+    int vmax = -1, ubest = 0, vbest = 0;  // this thread's first maximum
+    const int nstrips = cov ? (RY + kStrip - 1) / kStrip : 0;
+    for (int st = 0; st < nstrips; ++st) {
+      const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
+      // ---- row pass: g of the strip's 32 cells of row u
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int u = tid + q * kDtThreads;
+        if (u >= RX) {  // padding rows: no covered cell
+          if (u < RXP) {
+            uint32_t* grow = reinterpret_cast<uint32_t*>(G + u * kStrip);
+#pragma unroll
+            for (int j = 0; j < kStrip / 2; ++j) grow[j] = 0xFFFFFFFFu;
+          }
+          continue;
+        }
+        const uint64_t cw = Cb[u * RW + w];
+        const uint32_t sb = (uint32_t)(cw >> (32 * h));
+        // first covered column right of the strip
+        int firstR = kInf;
+        const uint32_t hb = h ? 0u : (uint32_t)(cw >> 32);
+        if (hb) {
+          firstR = c0 + 32 + __ffs(hb) - 1;
+        } else {
+          if (nrw[q] <= w) {  // scan for the next non-empty word (amortised O(RW) per row)
+            int k = w + 1;
+            while (k < RW && Cb[u * RW + k] == 0) ++k;
+            nrw[q] = k;
+          }
+          if (nrw[q] < RW) firstR = 64 * nrw[q] + __ffsll((unsigned long long)Cb[u * RW + nrw[q]]) - 1;
+        }
+        // g of each cell: nearest covered column at or left of it / at or
+        // right of it (inside the strip by bit scans, else the carries)
+        uint32_t* grow = reinterpret_cast<uint32_t*>(G + u * kStrip);
+        const int lc = lastL[q];
+#pragma unroll 4
+        for (int j = 0; j < kStrip; j += 2) {
+          int gg[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
+            const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
+            const int left = le ? c0 + 31 - __clz(le) : lc;
+            const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
+            gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+          }
+          grow[j >> 1] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
+        }
+        if (sb) lastL[q] = c0 + 31 - __clz(sb);
+      }
+      __syncthreads();
+      // ---- column pass: this thread's chunk of column c0 + col into registers.
+      // u0 is made opaque per strip: the compiler would otherwise hoist kCL
+      // loop-invariant row predicates and addresses out of the strip loop
+      // (and spill them)
+      int u0 = u0c;
+      asm volatile("" : "+v"(u0));
+      int gv[kCL];
+      int pmin = kInf, smin = kInf;
+      uint16_t* gcol = G + u0 * kStrip + col;  // row u0 + i at gcol[i * kStrip]
+#pragma unroll
+      for (int i = 0; i < kCL; ++i) {
+        const int u = u0 + i;
+        gv[i] = (int)gcol[i * kStrip];
+        pmin = min(pmin, gv[i] - u);
+        smin = min(smin, gv[i] + u);
+      }
+      s_cpre[chunk * kStrip + col] = pmin;
+      s_csuf[chunk * kStrip + col] = smin;
+      __syncthreads();
+      int run = kInf, sfx = kInf;  // minima over the chunks before / after this one
+      for (int q = 0; q < kChunks; ++q) {
+        const int a = s_cpre[q * kStrip + col], b = s_csuf[q * kStrip + col];
+        if (q < chunk) run = min(run, a);
+        if (q > chunk) sfx = min(sfx, b);
+      }
+      // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u into the
+      // strip (this thread's own cells), then the prefix scan: d
+#pragma unroll
+      for (int i = kCL - 1; i >= 0; --i) {
+        const int u = u0 + i;
+        sfx = min(sfx, gv[i] + u);
+        gcol[i * kStrip] = (uint16_t)min(sfx - u, 0xFFFF);
+      }
+      const int v = c0 + col;
+      const bool vin = v < RY;
+#pragma unroll
+      for (int i = 0; i < kCL; ++i) {
+        const int u = u0 + i;
+        run = min(run, gv[i] - u);
+        const int d = min(u + run, (int)gcol[i * kStrip]);
+        if (vin && u < RX && d > vmax) {
+          vmax = d;
+          ubest = u;
+          vbest = v;
+        }
+        gcol[i * kStrip] = (uint16_t)min(d, 0xFFFF);
+      }
+      __syncthreads();
+      for (int t = tid; t < T; t += kDtThreads) {
+        int tu, tv;
+        target(t, tu, tv);
+        if (tu >= 0 && tu < RX && tv >= c0 && tv < c0 + kStrip && tv < RY)
+          s_d[t] = (int)G[tu * kStrip + (tv - c0)];
+      }
+      __syncthreads();
+    }
+    // witness: of the maxima, the one farthest from the robot (new coverage
+    // comes from around the robot, so it keeps M valid longest)
+    if (cov && vmax >= 0) {
+      const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
+      atomicMax(&s_key, ((unsigned long long)vmax << 40) | ((unsigned long long)far << 24) |
+                            ((unsigned long long)ubest << 12) | (unsigned long long)vbest);
     }
     __syncthreads();
-  }
-  // witness: of the maxima, the one farthest from the robot (new coverage
-  // comes from around the robot, so it keeps M valid longest)
-  if (cov && vmax >= 0) {
-    const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
-    atomicMax(&s_key, ((unsigned long long)vmax << 40) | ((unsigned long long)far << 24) |
-                          ((unsigned long long)ubest << 12) | (unsigned long long)vbest);
-  }
-  __syncthreads();
-  // no covered cell: the restatement's convention (-1 everywhere); only the
-  // discarded reset-time PRE term can see it
-  const int M = cov ? (int)(s_key >> 40) : -1;
-  const float Mf = (float)M;
-  if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
-    const int wu = (int)((s_key >> 12) & 0xFFF), wv = (int)(s_key & 0xFFF);
-    reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
-  }
-  if (post) {
-    float* dst = dist_obs + ((size_t)e * s.N + a) * E * E;
-    for (int t = 5 + tid; t < T; t += kDtThreads)
-      dst[t - 5] = dist_value((float)(cov ? s_d[t] : -1), Mf);
-  }
-  float* pd = pre_out + ((size_t)e * s.N + a) * 8;
-  if (tid == 0) pd[0] = Mf;
-  if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
-  __syncthreads();  // the LDS is reused by the next item
+    // no covered cell: the restatement's convention (-1 everywhere); only the
+    // discarded reset-time PRE term can see it
+    const int M = cov ? (int)(s_key >> 40) : -1;
+    const float Mf = (float)M;
+    if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
+      const int wu = (int)((s_key >> 12) & 0xFFF), wv = (int)(s_key & 0xFFF);
+      reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
+    }
+    if (post) {
+      float* dst = dist_obs + (size_t)ea * E * E;
+      for (int t = 5 + tid; t < T; t += kDtThreads)
+        dst[t - 5] = dist_value((float)(cov ? s_d[t] : -1), Mf);
+    }
+    float* pd = pre_out + (size_t)ea * 8;
+    if (tid == 0) pd[0] = Mf;
+    if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
+    __syncthreads();  // the LDS is reused by the next item
   }
 }
 
 size_t dist_lds_bytes(const State& s, int pad) {
-  const size_t RX = s.Wp + 2 * pad, RW = (s.Lp + 2 * pad + 63) / 64;
-  // the strip area also stages the agent's MT tiles before the strips
-  const size_t strip = RX * kStrip * 4, tiles = (size_t)s.MT * 8;
-  return RX * RW * 8 + 2 * RX * RW * 4 + (strip > tiles ? strip : tiles);
+  return dt_lds(s.Wp + 2 * pad, s.Lp + 2 * pad, s.MT, 5 + s.E * s.E).total;
+}
+
+int dist_max_rows() { return kMaxRows; }
+
+// the instantiation whose register chunk holds ceil(RX / kChunks) rows
+static hipError_t launch_full(const State& s, int pad, int post, float* pre_out, float* dist_obs,
+                              const uint32_t* list, const uint32_t* count, unsigned grid,
+                              hipStream_t stream) {
+  const int RX = s.Wp + 2 * pad, cl = chunk_rows(RX);
+  const size_t lds = dist_lds_bytes(s, pad);
+#define MC_DT(CL)                                                                              \
+  do {                                                                                         \
+    if (lds > 65536) {                                                                         \
+      hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(&dist_kernel_t<CL>),   \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      if (e_ != hipSuccess) return e_;                                                         \
+    }                                                                                          \
+    hipLaunchKernelGGL(dist_kernel_t<CL>, dim3(grid), dim3(kDtThreads), lds, stream, s, pad,   \
+                       post, pre_out, dist_obs, list, count);                                  \
+  } while (0)
+  if (cl == 16) MC_DT(16);
+  else if (cl == 33) MC_DT(33);
+  else MC_DT(52);  // kMaxRows / kChunks
+#undef MC_DT
+  return hipGetLastError();
 }
 
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream) {
-  hipLaunchKernelGGL(dist_kernel, dim3((unsigned)((size_t)s.B * s.N)), dim3(kDtThreads),
-                     dist_lds_bytes(s, pad), stream, s, pad, post, pre_out, dist_obs,
-                     (const uint32_t*)nullptr, (const uint32_t*)nullptr);
-  return hipGetLastError();
+  return launch_full(s, pad, post, pre_out, dist_obs, nullptr, nullptr,
+                     (unsigned)((size_t)s.B * s.N), stream);
 }
 
 // --------------------------------------------------------------------------
@@ -338,9 +419,7 @@ hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist
   err = hipGetLastError();
   if (err != hipSuccess) return err;
   const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
-  hipLaunchKernelGGL(dist_kernel, dim3(grid), dim3(kDtThreads), dist_lds_bytes(s, pad), stream, s,
-                     pad, 1, pre_out, dist_obs, (const uint32_t*)list, (const uint32_t*)count);
-  return hipGetLastError();
+  return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, stream);
 }
 
 }  // namespace mc
