@@ -52,6 +52,8 @@ constexpr int kStrip = 32;                     // columns per strip
 constexpr int kChunks = kDtThreads / kStrip;   // row chunks per column in the column pass
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
+constexpr int kRowOff = 1024;                  // min(g - u) + kRowOff >= 0 (u < kMaxRows)
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
 // rows per column chunk: the instantiation (16, 33 or 52) whose kChunks
@@ -70,7 +72,7 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   L.cb = (size_t)RX * RW * 8;
   const size_t st = (size_t)kChunks * chunk_rows(RX) * kStrip * 2, tiles = (size_t)MT * 8;
   L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
-  L.mins = (size_t)2 * kChunks * kStrip * 4;
+  L.mins = (size_t)kChunks * kStrip * 4;
   L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
   L.total = L.cb + L.strip + L.mins + L.tgt;
   return L;
@@ -93,8 +95,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
   uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kStrip]
   constexpr int RXP = kChunks * kCL;                         // strip rows incl. padding
-  int* s_cpre = reinterpret_cast<int*>(smem + LL.cb + LL.strip);  // [kChunks][kStrip]
-  int* s_csuf = s_cpre + kChunks * kStrip;
+  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [kStrip][kChunks]
   int* s_d = reinterpret_cast<int*>(smem + LL.cb + LL.strip + LL.mins);
   const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
@@ -149,20 +150,25 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     int nrw[2] = {-1, -1};          // next non-empty word after the current one (-1: not scanned)
     const int col = tid % kStrip, chunk = tid / kStrip;
     const int u0c = chunk * kCL;
-    int vmax = -1, ubest = 0, vbest = 0;  // this thread's first maximum
+    // best (d << 16 | u) of this thread and its column (ties: the largest u)
+    uint32_t bestkey = 0;
+    int bestv = -1;
+    // bounding box of the target cells (extended coordinates): the column
+    // chunks inside it keep their d in the strip for the target reads
+    const int tu_lo = min(px - 1, px + pad - s.ego), tu_hi = max(px + 1, px + pad + s.ego);
+    const int tv_lo = min(py - 1, py + pad - s.ego), tv_hi = max(py + 1, py + pad + s.ego);
     const int nstrips = cov ? (RY + kStrip - 1) / kStrip : 0;
     for (int st = 0; st < nstrips; ++st) {
       const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
-      // ---- row pass: g of the strip's 32 cells of row u
+      // ---- row pass: g of the strip's 32 cells of row u, as 16 u16 pairs
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int u = tid + q * kDtThreads;
+        if (u >= RXP) continue;
+        uint4* grow = reinterpret_cast<uint4*>(G + u * kStrip);
         if (u >= RX) {  // padding rows: no covered cell
-          if (u < RXP) {
-            uint32_t* grow = reinterpret_cast<uint32_t*>(G + u * kStrip);
 #pragma unroll
-            for (int j = 0; j < kStrip / 2; ++j) grow[j] = 0xFFFFFFFFu;
-          }
+          for (int k = 0; k < 4; ++k) grow[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
           continue;
         }
         const uint64_t cw = Cb[u * RW + w];
@@ -180,30 +186,49 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           }
           if (nrw[q] < RW) firstR = 64 * nrw[q] + __ffsll((unsigned long long)Cb[u * RW + nrw[q]]) - 1;
         }
-        // g of each cell: nearest covered column at or left of it / at or
-        // right of it (inside the strip by bit scans, else the carries)
-        uint32_t* grow = reinterpret_cast<uint32_t*>(G + u * kStrip);
         const int lc = lastL[q];
-#pragma unroll 4
-        for (int j = 0; j < kStrip; j += 2) {
-          int gg[2];
+        uint32_t pk[kStrip / 2];
+        if (sb == 0u) {
+          // no covered cell in the strip: g(j) = min(A + j, B - j), two cells per packed op
+          const uint32_t A = (uint32_t)min(c0 - lc, 0xFFFF - kStrip);
+          const uint32_t Bd = (uint32_t)min(firstR - c0, 0xFFFF);  // >= 32
+          const u16x2 Ap = {(uint16_t)A, (uint16_t)A}, Bp = {(uint16_t)Bd, (uint16_t)Bd};
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
-            const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
-            const int left = le ? c0 + 31 - __clz(le) : lc;
-            const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
-            gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+          for (int jp = 0; jp < kStrip / 2; ++jp) {
+            const u16x2 cj = {(uint16_t)(2 * jp), (uint16_t)(2 * jp + 1)};
+            const u16x2 g = __builtin_elementwise_min(Ap + cj, Bp - cj);
+            pk[jp] = __builtin_bit_cast(uint32_t, g);
           }
-          grow[j >> 1] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
+        } else if (sb == ~0u) {
+#pragma unroll
+          for (int jp = 0; jp < kStrip / 2; ++jp) pk[jp] = 0u;
+        } else {
+          // g of each cell: nearest covered column at or left of it / at or
+          // right of it (inside the strip by bit scans, else the carries)
+#pragma unroll
+          for (int j = 0; j < kStrip; j += 2) {
+            int gg[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
+              const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
+              const int left = le ? c0 + 31 - __clz(le) : lc;
+              const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
+              gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+            }
+            pk[j >> 1] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
+          }
+          lastL[q] = c0 + 31 - __clz(sb);
         }
-        if (sb) lastL[q] = c0 + 31 - __clz(sb);
+        if (sb == ~0u) lastL[q] = c0 + 31;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          grow[k] = make_uint4(pk[4 * k], pk[4 * k + 1], pk[4 * k + 2], pk[4 * k + 3]);
       }
       __syncthreads();
       // ---- column pass: this thread's chunk of column c0 + col into registers.
       // u0 is made opaque per strip: the compiler would otherwise hoist kCL
-      // loop-invariant row predicates and addresses out of the strip loop
-      // (and spill them)
+      // loop-invariant row values out of the strip loop (and spill them)
       int u0 = u0c;
       asm volatile("" : "+v"(u0));
       int gv[kCL];
@@ -211,41 +236,67 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       uint16_t* gcol = G + u0 * kStrip + col;  // row u0 + i at gcol[i * kStrip]
 #pragma unroll
       for (int i = 0; i < kCL; ++i) {
-        const int u = u0 + i;
         gv[i] = (int)gcol[i * kStrip];
-        pmin = min(pmin, gv[i] - u);
-        smin = min(smin, gv[i] + u);
+        pmin = min(pmin, gv[i] - (u0 + i));
+        smin = min(smin, gv[i] + (u0 + i));
       }
-      s_cpre[chunk * kStrip + col] = pmin;
-      s_csuf[chunk * kStrip + col] = smin;
+      // chunk minima, packed: low half min(g - u) + RXOFF, high half min(g + u)
+      s_cmin[col * kChunks + chunk] =
+          (uint32_t)min(pmin + kRowOff, 0xFFFF) | ((uint32_t)min(smin, 0xFFFF) << 16);
       __syncthreads();
-      int run = kInf, sfx = kInf;  // minima over the chunks before / after this one
-      for (int q = 0; q < kChunks; ++q) {
-        const int a = s_cpre[q * kStrip + col], b = s_csuf[q * kStrip + col];
-        if (q < chunk) run = min(run, a);
-        if (q > chunk) sfx = min(sfx, b);
+      u16x2 accP = {0xFFFF, 0xFFFF}, accS = {0xFFFF, 0xFFFF};
+      {
+        const uint4* cm = reinterpret_cast<const uint4*>(s_cmin + col * kChunks);
+#pragma unroll
+        for (int k = 0; k < kChunks / 4; ++k) {
+          const uint4 q4 = cm[k];
+          const uint32_t qv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+          for (int l = 0; l < 4; ++l) {
+            const int q = 4 * k + l;
+            const u16x2 val = __builtin_bit_cast(u16x2, qv[l]);
+            const u16x2 none = {0xFFFF, 0xFFFF};
+            accP = __builtin_elementwise_min(accP, q < chunk ? val : none);
+            accS = __builtin_elementwise_min(accS, q > chunk ? val : none);
+          }
+        }
       }
-      // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u into the
-      // strip (this thread's own cells), then the prefix scan: d
+      // minima over the chunks before / after this one
+      int run = (int)accP.x - kRowOff, sfx = (int)accS.y;
+      if (accP.x == 0xFFFF) run = kInf;
+      if (accS.y == 0xFFFF) sfx = kInf;
+      // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u
+      int dn[kCL];
 #pragma unroll
       for (int i = kCL - 1; i >= 0; --i) {
-        const int u = u0 + i;
-        sfx = min(sfx, gv[i] + u);
-        gcol[i * kStrip] = (uint16_t)min(sfx - u, 0xFFFF);
+        sfx = min(sfx, gv[i] + (u0 + i));
+        dn[i] = sfx - (u0 + i);
       }
       const int v = c0 + col;
-      const bool vin = v < RY;
+      const bool keep = v >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
+      uint32_t key = 0;
+      if (u0 + kCL <= RX) {
 #pragma unroll
-      for (int i = 0; i < kCL; ++i) {
-        const int u = u0 + i;
-        run = min(run, gv[i] - u);
-        const int d = min(u + run, (int)gcol[i * kStrip]);
-        if (vin && u < RX && d > vmax) {
-          vmax = d;
-          ubest = u;
-          vbest = v;
+        for (int i = 0; i < kCL; ++i) {
+          run = min(run, gv[i] - (u0 + i));
+          gv[i] = min(u0 + i + run, dn[i]);  // d
+          key = max(key, ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i));
         }
-        gcol[i * kStrip] = (uint16_t)min(d, 0xFFFF);
+      } else {  // the chunk with the padding rows
+#pragma unroll
+        for (int i = 0; i < kCL; ++i) {
+          run = min(run, gv[i] - (u0 + i));
+          gv[i] = min(u0 + i + run, dn[i]);
+          if (u0 + i < RX) key = max(key, ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i));
+        }
+      }
+      if (v < RY && key > bestkey) {
+        bestkey = key;
+        bestv = v;
+      }
+      if (keep) {
+#pragma unroll
+        for (int i = 0; i < kCL; ++i) gcol[i * kStrip] = (uint16_t)min(gv[i], 0xFFFF);
       }
       __syncthreads();
       for (int t = tid; t < T; t += kDtThreads) {
@@ -256,6 +307,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       }
       __syncthreads();
     }
+    const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
+    const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
     // witness: of the maxima, the one farthest from the robot (new coverage
     // comes from around the robot, so it keeps M valid longest)
     if (cov && vmax >= 0) {
