@@ -72,7 +72,7 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   L.cb = (size_t)RX * RW * 8;
   const size_t st = (size_t)kChunks * chunk_rows(RX) * kStrip * 2, tiles = (size_t)MT * 8;
   L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
-  L.mins = (size_t)kChunks * kStrip * 4;
+  L.mins = (size_t)2 * kChunks * kStrip * 4;
   L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
   L.total = L.cb + L.strip + L.mins + L.tgt;
   return L;
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
   uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kStrip]
   constexpr int RXP = kChunks * kCL;                         // strip rows incl. padding
-  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [kStrip][kChunks]
+  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [2][kStrip][kChunks]
   int* s_d = reinterpret_cast<int*>(smem + LL.cb + LL.strip + LL.mins);
   const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
@@ -241,12 +241,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         smin = min(smin, gv[i] + (u0 + i));
       }
       // chunk minima, packed: low half min(g - u) + RXOFF, high half min(g + u)
-      s_cmin[col * kChunks + chunk] =
+      uint32_t* cmin = s_cmin + (st & 1) * (kChunks * kStrip);  // double buffer: 2 barriers per strip
+      cmin[col * kChunks + chunk] =
           (uint32_t)min(pmin + kRowOff, 0xFFFF) | ((uint32_t)min(smin, 0xFFFF) << 16);
       __syncthreads();
       u16x2 accP = {0xFFFF, 0xFFFF}, accS = {0xFFFF, 0xFFFF};
       {
-        const uint4* cm = reinterpret_cast<const uint4*>(s_cmin + col * kChunks);
+        const uint4* cm = reinterpret_cast<const uint4*>(cmin + col * kChunks);
 #pragma unroll
         for (int k = 0; k < kChunks / 4; ++k) {
           const uint4 q4 = cm[k];
@@ -266,46 +267,44 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (accP.x == 0xFFFF) run = kInf;
       if (accS.y == 0xFFFF) sfx = kInf;
       // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u
-      int dn[kCL];
+      // (u16 pairs: register budget of two workgroups per CU)
+      uint32_t dnp[(kCL + 1) / 2];
 #pragma unroll
       for (int i = kCL - 1; i >= 0; --i) {
         sfx = min(sfx, gv[i] + (u0 + i));
-        dn[i] = sfx - (u0 + i);
+        const uint32_t dn = (uint32_t)min(sfx - (u0 + i), 0xFFFF);
+        if (i & 1) dnp[i >> 1] = dn << 16;
+        else dnp[i >> 1] = (i + 1 < kCL ? dnp[i >> 1] : 0u) | dn;
       }
       const int v = c0 + col;
       const bool keep = v >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
       uint32_t key = 0;
-      if (u0 + kCL <= RX) {
+      // rows of this chunk inside the grid (only the last chunk has padding)
+      const int nin = max(RX - u0, 0);
+      const uint64_t vm = nin >= kCL ? ~0ull : ((1ull << nin) - 1ull);
 #pragma unroll
-        for (int i = 0; i < kCL; ++i) {
-          run = min(run, gv[i] - (u0 + i));
-          gv[i] = min(u0 + i + run, dn[i]);  // d
-          key = max(key, ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i));
-        }
-      } else {  // the chunk with the padding rows
-#pragma unroll
-        for (int i = 0; i < kCL; ++i) {
-          run = min(run, gv[i] - (u0 + i));
-          gv[i] = min(u0 + i + run, dn[i]);
-          if (u0 + i < RX) key = max(key, ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i));
-        }
+      for (int i = 0; i < kCL; ++i) {
+        run = min(run, gv[i] - (u0 + i));
+        gv[i] = min(u0 + i + run, (int)((dnp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu));  // d
+        const uint32_t k = ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i);
+        key = max(key, ((vm >> i) & 1ull) ? k : 0u);
       }
       if (v < RY && key > bestkey) {
         bestkey = key;
         bestv = v;
       }
-      if (keep) {
+      if (keep) {  // the target cells of this column chunk, from registers
+        for (int t = 0; t < T; ++t) {
+          int tu, tv;
+          target(t, tu, tv);
+          if (tv == v && tu >= u0 && tu < u0 + kCL && tu < RX) {
+            int val = 0;
 #pragma unroll
-        for (int i = 0; i < kCL; ++i) gcol[i * kStrip] = (uint16_t)min(gv[i], 0xFFFF);
+            for (int i = 0; i < kCL; ++i) val = (u0 + i == tu) ? gv[i] : val;
+            s_d[t] = min(val, 0xFFFF);
+          }
+        }
       }
-      __syncthreads();
-      for (int t = tid; t < T; t += kDtThreads) {
-        int tu, tv;
-        target(t, tu, tv);
-        if (tu >= 0 && tu < RX && tv >= c0 && tv < c0 + kStrip && tv < RY)
-          s_d[t] = (int)G[tu * kStrip + (tv - c0)];
-      }
-      __syncthreads();
     }
     const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
     const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
