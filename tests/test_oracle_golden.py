@@ -5,6 +5,9 @@ import pytest
 
 from golden_util import GOLDEN_DIR, case_names, check_against_golden, load_case, make_env, replay
 from oracle.cpu_ref import DecGridRLRef, lidar_beam_table, lidar_thetas
+from oracle.super_ref import SuperGridRLRef
+from super_golden_util import (check_super_golden, load_super_case, make_super_env, replay_super,
+                               super_case_names)
 
 
 @pytest.mark.parametrize("name", case_names())
@@ -20,6 +23,24 @@ def test_beam_table_bits():
         b = int(key[1:])
         tab = lidar_beam_table(lidar_thetas(b))
         np.testing.assert_array_equal(tab.view(np.uint64), z[key].view(np.uint64), err_msg=key)
+
+
+@pytest.mark.parametrize("name", super_case_names())
+def test_super_oracle_matches_reference_golden(name):
+    case = load_super_case(name)
+    env = make_super_env(SuperGridRLRef, case)
+    replay_super(env, case, check_super_golden(env))
+
+
+def test_super_golden_inventory():
+    names = super_case_names()
+    assert len(names) >= 9
+    # the captured runs exercise done (terminal reward), done_incr, sentinels
+    # and every motion-penalty quotient
+    done_any = [bool(load_super_case(n)["done"].any()) for n in names]
+    assert sum(done_any) >= 2
+    q = load_super_case("sg_sentinels_quotients_n2")
+    assert set(q["a_prev"].tolist()) >= {0, 1, 2, 3}
 
 
 def test_golden_inventory():
