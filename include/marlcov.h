@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 3
+#define MARLCOV_ABI_VERSION 4
 
 enum {
   MC_OK = 0,
@@ -132,8 +132,9 @@ enum {
 
 int32_t mc_abi_version(void);
 const char* mc_last_error(void);
-/* sizeof(mc_config) (which=0) / sizeof(mc_layout) (which=1): lets an FFI
- * binding verify its struct mirror. */
+/* sizeof(mc_config) (which=0) / sizeof(mc_layout) (1) / sizeof(mc_sg_config)
+ * (2) / sizeof(mc_sg_layout) (3): lets an FFI binding verify its struct
+ * mirrors. */
 int64_t mc_struct_size(int32_t which);
 
 /* Allocate device state for cfg->num_envs envs on HIP device `hip_device`.
@@ -192,6 +193,105 @@ int mc_set_dist_obs(void* env, float* dev_dist_obs);
 
 /* Synchronise `stream` and report (then clear) the device error word. */
 int mc_check(void* env, void* stream);
+
+/* ==========================================================================
+ * SuperGridRL — the centralized, fully observed env variant
+ * (Environments/super_grid_rl.py:18-463).  A separate
+ * handle type with the same conventions as above, except that grids are NOT
+ * padded (SuperGridRL never pads, :357-366) and maps are row bitboards:
+ * uint64 [W][ceil(L/64)], bit (y & 63) of word (x, y >> 6) = cell (x, y).
+ *
+ * The state the reference returns from every reset/step (get_state,
+ * :305-317: P position layers, observed obstacles, _free, distance map) lives
+ * in two caller buffers registered with mc_sg_set_obs and MAINTAINED by the
+ * library: reset rewrites them whole, a step updates only the cells it
+ * changes (robot cells, sensed windows) and rewrites the distance layer.  The
+ * caller reads them and must not write them.
+ * ======================================================================== */
+
+typedef struct mc_sg_config {
+  int32_t num_envs;           /* B (batch extra)                              */
+  int32_t num_agents;         /* 'numrobot', 1..64                            */
+  int32_t width;              /* grid rows W (unpadded)                       */
+  int32_t length;             /* grid columns L (unpadded)                    */
+  int32_t num_grids;          /* G grids in the device pool (>= 1)            */
+  int32_t senseradius;        /* 'senseradius', 0..15                         */
+  double collision_penalty;   /* 'collision_penalty'                          */
+  double free_penalty;        /* 'free_penalty'                               */
+  double terminal_reward;     /* 'terminal_reward'                            */
+  double done_thresh;         /* 'done_thresh' (initial, per env)             */
+  double done_incr;           /* 'done_incr'                                  */
+  int32_t dist_reward;        /* 'dist_reward'                                */
+  int32_t use_scanning;       /* 'use_scanning' (one position layer)          */
+  int32_t maxsteps;           /* batch extra: done when currstep == maxsteps
+                                 (the episode cut of Utils/utils.py:25-28);
+                                 0 = never, as in SuperGridRL.done()         */
+  int32_t auto_reset;         /* batch extra: reset an env that reports done  */
+  int32_t reset_grid_mode;    /* 0: keep the env's grid; 1: draw from the pool */
+  int32_t pad_;
+  uint64_t seed;              /* batch extra: device Philox seed              */
+} mc_sg_config;
+
+typedef struct mc_sg_layout {
+  int32_t pos_layers;         /* P: N, or 1 with use_scanning (:330-341)      */
+  int32_t obs_layers;         /* P + 2 uint8 layers (positions, obstacles, free) */
+  int32_t row_words;          /* ceil(L / 64)                                 */
+  int32_t pad_;
+  int64_t state_bytes;        /* device bytes owned by the handle             */
+} mc_sg_layout;
+
+enum {
+  MC_SG_FIELD_POS = 0,        /* int32  [B][N][2] (_xinds, _yinds)            */
+  MC_SG_FIELD_COVERED = 1,    /* uint64 [B][W][RW] _free == 0 (sensed)        */
+  MC_SG_FIELD_OBST = 2,       /* uint64 [B][W][RW] _observed_obstacles        */
+  MC_SG_FIELD_COV_COUNT = 3,  /* uint32 [B] count_nonzero(_free < 1)          */
+  MC_SG_FIELD_CURRSTEP = 4,   /* int32  [B] _currstep                         */
+  MC_SG_FIELD_DONE_THRESH = 5,/* double [B] _done_thresh                      */
+  MC_SG_FIELD_A_PREV = 6,     /* int32  [B] a_prev (-1 = None)                */
+  MC_SG_FIELD_ENV_GRID = 7,   /* int32  [B] grid pool index                   */
+  MC_SG_FIELD_EPISODE = 8,    /* uint32 [B] resets so far (RNG counter)       */
+  MC_SG_FIELD_NUMPOS = 9,     /* int32  [G] count_nonzero(grid > 0)           */
+  MC_SG_FIELD_GRID_NEG = 10,  /* uint64 [G][W][RW] grid < 0                   */
+  MC_SG_FIELD_GRID_POS = 11,  /* uint64 [G][W][RW] grid > 0                   */
+  MC_SG_FIELD_COUNT = 12
+};
+
+/* Replaces SuperGridRL.__init__ (:27-72) minus the first reset. */
+int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env);
+void mc_sg_destroy(void* env);
+int mc_sg_query(void* env, mc_sg_layout* out);
+/* dev_grids int8 [num_grids][W][L], values < 0 obstacle, 0, > 0 free. */
+int mc_sg_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void* stream);
+/* Bernoulli pool: every cell an obstacle with probability p_obst (gridgen's
+ * distribution, Utils/gridmaker.py:127-128; not its bits). */
+int mc_sg_generate_grids(void* env, uint64_t seed, double p_obst, void* stream);
+int mc_sg_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream);
+/* Register the state buffers (see above): dev_planes uint8 [B][P+2][W][L]
+ * (layers 0..P-1 robot positions, P observed obstacles, P+1 _free),
+ * dev_dist float32 [B][W][L] (get_distance_map, :281-303).  Required before
+ * the first reset. */
+int mc_sg_set_obs(void* env, uint8_t* dev_planes, float* dev_dist);
+/* SuperGridRL.reset (:343-399) of the envs with dev_env_mask[e] != 0 (NULL =
+ * all): start cells injected (dev_pos int32 [B][N][2]) or drawn on the device
+ * (Philox rejection, the acceptance rule of :378-388); _done_thresh and
+ * a_prev are kept, as in the reference. */
+int mc_sg_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, void* stream);
+/* SuperGridRL.step (:74-225) of every env.  dev_actions uint8 [B][N]: the
+ * base-4 digits of the joint action, slot 0 first (:93-98); 0 = x-1, 1 = x+1,
+ * 2 = y+1, 3 = y-1 (:131-174); 4..254 no-op; 255 in slot 0 = the sentinel
+ * path (:88-90: reward 0, done, no state change).  dev_quot int32 [B]
+ * (nullable = all 0): action // 4**N, the value motion_penalty sees (:203-208);
+ * >= 4 raises the device error (the reference's KeyError).  Writes reward
+ * float64 [B] and done uint8 [B], and updates the registered state buffers. */
+int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, double* dev_reward,
+               uint8_t* dev_done, void* stream);
+int64_t mc_sg_field_bytes(void* env, int32_t field);
+int mc_sg_get_state(void* env, int32_t field, void* dev_dst, int64_t bytes, void* stream);
+/* Uploads mark the state buffers for a full rewrite at the next call. */
+int mc_sg_set_state(void* env, int32_t field, const void* dev_src, int64_t bytes, void* stream);
+/* Synchronise and report (then clear) the device error word:
+ * 4 = placement failed, 8 = bad injected cell, 16 = motion_penalty KeyError. */
+int mc_sg_check(void* env, void* stream);
 
 /* Diagnostics: in a -DMC_STAMPS build, record per-phase s_memtime stamps of
  * every env into dev_stamps uint64 [B][16]; MC_EINVAL in normal builds. */

@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
@@ -70,6 +70,48 @@ class McLayout(ctypes.Structure):
     ]
 
 
+class McSgConfig(ctypes.Structure):
+    """Mirror of ``mc_sg_config`` (SuperGridRL handles)."""
+
+    _fields_ = [
+        ("num_envs", ctypes.c_int32),
+        ("num_agents", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("length", ctypes.c_int32),
+        ("num_grids", ctypes.c_int32),
+        ("senseradius", ctypes.c_int32),
+        ("collision_penalty", ctypes.c_double),
+        ("free_penalty", ctypes.c_double),
+        ("terminal_reward", ctypes.c_double),
+        ("done_thresh", ctypes.c_double),
+        ("done_incr", ctypes.c_double),
+        ("dist_reward", ctypes.c_int32),
+        ("use_scanning", ctypes.c_int32),
+        ("maxsteps", ctypes.c_int32),
+        ("auto_reset", ctypes.c_int32),
+        ("reset_grid_mode", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class McSgLayout(ctypes.Structure):
+    """Mirror of ``mc_sg_layout``."""
+
+    _fields_ = [
+        ("pos_layers", ctypes.c_int32),
+        ("obs_layers", ctypes.c_int32),
+        ("row_words", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("state_bytes", ctypes.c_int64),
+    ]
+
+
+(SG_FIELD_POS, SG_FIELD_COVERED, SG_FIELD_OBST, SG_FIELD_COV_COUNT, SG_FIELD_CURRSTEP,
+ SG_FIELD_DONE_THRESH, SG_FIELD_A_PREV, SG_FIELD_ENV_GRID, SG_FIELD_EPISODE, SG_FIELD_NUMPOS,
+ SG_FIELD_GRID_NEG, SG_FIELD_GRID_POS) = range(12)
+
+
 # (name, restype, argtypes) for every symbol include/marlcov.h declares
 _VP, _I32, _I64, _U64, _D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 SIGNATURES = [
@@ -91,6 +133,19 @@ SIGNATURES = [
     ("mc_check", ctypes.c_int, [_VP, _VP]),
     ("mc_debug_stamps", ctypes.c_int, [_VP, _VP]),
     ("mc_set_dist_obs", ctypes.c_int, [_VP, _VP]),
+    ("mc_sg_create", ctypes.c_int, [ctypes.POINTER(McSgConfig), ctypes.c_int, ctypes.POINTER(_VP)]),
+    ("mc_sg_destroy", None, [_VP]),
+    ("mc_sg_query", ctypes.c_int, [_VP, ctypes.POINTER(McSgLayout)]),
+    ("mc_sg_set_grids", ctypes.c_int, [_VP, _VP, _I32, _VP]),
+    ("mc_sg_generate_grids", ctypes.c_int, [_VP, _U64, _D, _VP]),
+    ("mc_sg_set_env_grids", ctypes.c_int, [_VP, _VP, _VP]),
+    ("mc_sg_set_obs", ctypes.c_int, [_VP, _VP, _VP]),
+    ("mc_sg_reset", ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    ("mc_sg_step", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    ("mc_sg_field_bytes", _I64, [_VP, _I32]),
+    ("mc_sg_get_state", ctypes.c_int, [_VP, _I32, _VP, _I64, _VP]),
+    ("mc_sg_set_state", ctypes.c_int, [_VP, _I32, _VP, _I64, _VP]),
+    ("mc_sg_check", ctypes.c_int, [_VP, _VP]),
 ]
 
 _lib = None
@@ -117,8 +172,9 @@ def load(path: str | None = None):
         fn.argtypes = args
     if lib.mc_abi_version() != ABI_VERSION:
         raise ImportError(f"libmarlcov ABI {lib.mc_abi_version()} != expected {ABI_VERSION}")
-    if lib.mc_struct_size(0) != ctypes.sizeof(McConfig) or lib.mc_struct_size(1) != ctypes.sizeof(McLayout):
-        raise ImportError("libmarlcov struct layout mismatch (mc_config / mc_layout)")
+    mirrors = (McConfig, McLayout, McSgConfig, McSgLayout)
+    if any(lib.mc_struct_size(i) != ctypes.sizeof(m) for i, m in enumerate(mirrors)):
+        raise ImportError("libmarlcov struct layout mismatch (mc_config / mc_layout / mc_sg_*)")
     _lib = lib
     return lib
 

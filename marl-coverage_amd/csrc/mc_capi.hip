@@ -142,6 +142,11 @@ int launch_epw(const Env* E) {
 
 }  // namespace
 
+namespace mc {
+// shared with mc_super.hip: one thread-local message for mc_last_error()
+void set_last_error(const char* msg) { g_err = msg; }
+}  // namespace mc
+
 extern "C" {
 
 int32_t mc_abi_version(void) { return MARLCOV_ABI_VERSION; }
@@ -152,6 +157,8 @@ int64_t mc_struct_size(int32_t which) {
   switch (which) {
     case 0: return (int64_t)sizeof(mc_config);
     case 1: return (int64_t)sizeof(mc_layout);
+    case 2: return (int64_t)sizeof(mc_sg_config);
+    case 3: return (int64_t)sizeof(mc_sg_layout);
     default: return -1;
   }
 }

@@ -1,0 +1,899 @@
+// mc_super.hip — batched SuperGridRL, the centralized fully observed env
+// (Environments/super_grid_rl.py:18-463), and its
+// extern "C" entry points (include/marlcov.h, mc_sg_*).
+//
+// Per step (mc_sg_step), two kernels on the caller's stream:
+//   sg_step_kernel  one wave per env: scan order (:108-129), sequential moves
+//                   with live occupancy (:121-174), the square sense windows
+//                   in robot order with the reference's per-slot float64
+//                   reward folds (:177-201), motion penalty (:203-208,
+//                   227-243), np.sum of the slots (pairwise, :214), terminal
+//                   reward and done (:215-223, 401-421), and the incremental
+//                   update of the registered state planes (robot cells, the
+//                   sensed windows of the obstacle / _free layers);
+//   sg_dist_kernel  one workgroup per env: get_distance_map (:281-303) of the
+//                   post-step _free map — exact L1 distance of every cell to
+//                   the nearest cell with _free != 0, separable: a row pass
+//                   (distance along the row) then a column pass (down/up
+//                   min-plus sweeps), then 1 - d / max(d) in float32 into the
+//                   dist layer.  That layer is also the NEXT step's pre-move
+//                   distance_map (:117-118): _free does not change between
+//                   get_state and the next get_distance_map, so the step
+//                   kernel reads its dist terms from it (no second transform).
+// Maps are row bitboards: uint64 [W][RW], RW = ceil(L/64); bits >= L of a
+// row's last word are always 0.
+//
+// The transform's OpenCV semantics follow the oracle's SciPy restatement
+// (oracle/super_ref.py): exact L1; with no source cell at all (an obstacle-
+// free grid fully covered) d is -1 everywhere, so the layer is 2.0 — parity
+// vs real cv2 unpinned.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <string>
+#include <vector>
+
+#include "marlcov.h"
+#include "mc_device.h"
+
+namespace mc {
+void set_last_error(const char* msg);
+}
+
+namespace mcs {
+
+using mc::bounded;
+using mc::dist_value;
+using mc::low_mask;
+using mc::philox;
+
+enum : uint32_t { ERR_PLACEMENT = 1u << 2, ERR_INJECT = 1u << 3, ERR_KEY = 1u << 4 };
+constexpr int kMaxAgents = 64;
+constexpr int kMaxRadius = 15;   // a window row (2r+1 cells) fits 32 bits
+constexpr int kMaxSide = 4096;
+constexpr int kEnvsPerBlock = 4; // step / reset kernels: one wave per env
+constexpr int kInfD = 0xFFFF;    // "no source" in the u16 distance planes
+constexpr size_t kLdsLimit = 64 * 1024;
+
+struct SState {
+  int B, N, W, L, G, RW, r, P;
+  double pen, fpen, term, dincr;
+  int dist, scan, maxsteps, auto_reset, grid_mode;
+  uint32_t mg_L;  // floor(i / L) == umulhi(i, mg_L) (L >= 2)
+  uint64_t seed;
+  const uint64_t* gneg;   // [G][W][RW] grid < 0
+  const uint64_t* gpos;   // [G][W][RW] grid > 0
+  const int32_t* numpos;  // [G] count_nonzero(grid > 0)
+  int32_t* env_grid;      // [B]
+  int32_t* pos;           // [B][N][2]
+  uint64_t* cov;          // [B][W][RW] sensed cells (_free == 0)
+  uint64_t* obst;         // [B][W][RW] _observed_obstacles
+  uint32_t* cov_cnt;      // [B] count_nonzero(_free < 1)
+  int32_t* currstep;      // [B]
+  double* done_thresh;    // [B]
+  int32_t* a_prev;        // [B] (-1 = None)
+  uint32_t* episode;      // [B]
+  uint8_t* full;          // [B] state planes need a full rewrite
+  uint32_t* err;
+  uint8_t* planes;        // caller: [B][P+2][W][L]
+  float* dist_plane;      // caller: [B][W][L]
+  uint16_t* scratch;      // [B][W][pitch] distance planes when they exceed LDS
+};
+
+__device__ __forceinline__ int div_L(const SState& s, int i) {
+  return s.L == 1 ? i : (int)__umulhi((uint32_t)i, s.mg_L);
+}
+
+__device__ __forceinline__ bool bit_at(const uint64_t* map, int RW, int x, int y) {
+  return (map[(size_t)x * RW + (y >> 6)] >> (y & 63)) & 1ull;
+}
+
+// bits [c0, c0 + 32) of a row (c0 may be negative; bit b = cell c0 + b)
+__device__ __forceinline__ uint32_t row_field(const uint64_t* row, int RW, int c0) {
+  const int w0 = c0 >> 6, sh = c0 & 63;  // arithmetic shift: floor
+  const uint64_t a = (w0 >= 0 && w0 < RW) ? row[w0] : 0ull;
+  const uint64_t b = (w0 + 1 >= 0 && w0 + 1 < RW) ? row[w0 + 1] : 0ull;
+  return (uint32_t)(sh ? (a >> sh) | (b << (64 - sh)) : a);
+}
+
+// OR field f (bit b = cell c0 + b; only in-row bits set) into a row
+__device__ __forceinline__ void or_field(uint64_t* row, int RW, int c0, uint32_t f) {
+  if (!f) return;
+  const int w0 = c0 >> 6, sh = c0 & 63;
+  const uint64_t F = f;
+  const uint64_t lo = F << sh, hi = sh ? F >> (64 - sh) : 0ull;
+  if (w0 >= 0 && lo) atomicOr((unsigned long long*)&row[w0], (unsigned long long)lo);
+  if (w0 + 1 < RW && hi) atomicOr((unsigned long long*)&row[w0 + 1], (unsigned long long)hi);
+}
+
+__device__ __forceinline__ uint32_t mask32(int lo, int hi) {  // bits [lo, hi), 0 <= lo, hi <= 32
+  if (hi <= lo) return 0u;
+  const uint32_t h = hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u);
+  return h & ~((1u << lo) - 1u);
+}
+
+// numpy's pairwise float64 sum of a contiguous array (n <= 128): what
+// np.sum(reward) computes at super_grid_rl.py:214
+__device__ double np_pairwise_sum(const double* a, int n) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// --------------------------------------------------------------------------
+// reset (:343-399) of env e by one wave: grid pick, zeroed maps, start cells
+// (injected, or Philox candidates x = randint(W), y = randint(L) consumed in
+// draw order with the reference's acceptance rule grid >= 0 and unoccupied,
+// :378-388).  _done_thresh and a_prev are kept (the reference never resets
+// them).  The state planes are flagged for a full rewrite.
+// --------------------------------------------------------------------------
+__device__ void sg_reset_env(const SState& s, int e, int lane, const int32_t* inj) {
+  const int N = s.N;
+  const uint32_t ep = s.episode[e] + 1u;
+  int g = s.env_grid[e];
+  if (s.grid_mode == 1) {
+    const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, (uint32_t)e, ep, 0x53677264u));
+    g = (int)bounded(r.x, (uint32_t)s.G);
+  }
+  const size_t mw = (size_t)s.W * s.RW;
+  uint64_t* cov = s.cov + (size_t)e * mw;
+  uint64_t* obst = s.obst + (size_t)e * mw;
+  for (size_t i = lane; i < mw; i += 64) {
+    cov[i] = 0ull;
+    obst[i] = 0ull;
+  }
+  const uint64_t* gneg = s.gneg + (size_t)g * mw;
+  int px = -1, py = -1;
+  if (inj != nullptr) {
+    if (lane < N) {
+      px = inj[((size_t)e * N + lane) * 2];
+      py = inj[((size_t)e * N + lane) * 2 + 1];
+      bool bad = px < 0 || py < 0 || px >= s.W || py >= s.L || bit_at(gneg, s.RW, px, py);
+      for (int j = 0; j < lane; ++j)
+        bad |= inj[((size_t)e * N + j) * 2] == px && inj[((size_t)e * N + j) * 2 + 1] == py;
+      if (bad) atomicOr(s.err, ERR_INJECT);
+    }
+  } else {
+    int placed = 0;
+    for (int round = 0; round < 4096 && placed < N; ++round) {
+      const uint32_t k = (uint32_t)(round * 64 + lane);
+      const uint4 r = philox(s.seed, make_uint4(k, (uint32_t)e, ep, 0x53706c63u));
+      const int cx = (int)bounded(r.x, (uint32_t)s.W);
+      const int cy = (int)bounded(r.y, (uint32_t)s.L);
+      uint64_t okm = __ballot(!bit_at(gneg, s.RW, cx, cy));
+      while (okm && placed < N) {
+        const int j = __ffsll((unsigned long long)okm) - 1;
+        okm &= okm - 1;
+        const int qx = __shfl(cx, j), qy = __shfl(cy, j);
+        const bool clash = __ballot(lane < placed && px == qx && py == qy) != 0ull;
+        if (!clash) {
+          if (lane == placed) {
+            px = qx;
+            py = qy;
+          }
+          ++placed;
+        }
+      }
+    }
+    if (placed < N && lane == 0) atomicOr(s.err, ERR_PLACEMENT);
+  }
+  if (lane < N) {
+    s.pos[((size_t)e * N + lane) * 2] = px;
+    s.pos[((size_t)e * N + lane) * 2 + 1] = py;
+  }
+  if (lane == 0) {
+    s.episode[e] = ep;
+    s.env_grid[e] = g;
+    s.cov_cnt[e] = 0;
+    s.currstep[e] = 0;
+    s.full[e] = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void sg_reset_kernel(SState s, const uint8_t* __restrict__ mask,
+                                                       const int32_t* __restrict__ inj) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6);
+  if (e >= s.B) return;
+  if (mask != nullptr && mask[e] == 0) return;
+  sg_reset_env(s, e, lane, inj);
+}
+
+// --------------------------------------------------------------------------
+// SuperGridRL.step (:74-225), one wave per env, lane i = robot i.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* __restrict__ actions,
+                                                      const int32_t* __restrict__ quot,
+                                                      double* __restrict__ reward,
+                                                      uint8_t* __restrict__ done) {
+  __shared__ double s_v[kEnvsPerBlock][kMaxAgents];
+  __shared__ int s_x[kEnvsPerBlock][kMaxAgents], s_y[kEnvsPerBlock][kMaxAgents];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * kEnvsPerBlock + w;
+  if (e >= s.B) return;
+  const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = s.r;
+  const bool me = lane < N;
+  bool is_done;
+  if (actions[(size_t)e * N] == 255) {  // action == -1 / None (:88-90)
+    is_done = true;
+    if (lane == 0) {
+      reward[e] = 0.0;
+      done[e] = 1;
+    }
+  } else {
+    const size_t mw = (size_t)W * RW;
+    const int g = s.env_grid[e];
+    const uint64_t* gneg = s.gneg + (size_t)g * mw;
+    const uint64_t* gpos = s.gpos + (size_t)g * mw;
+    uint64_t* cov = s.cov + (size_t)e * mw;
+    uint64_t* obst = s.obst + (size_t)e * mw;
+    int x = -(1 << 20), y = -(1 << 20);
+    if (me) {
+      x = s.pos[((size_t)e * N + lane) * 2];
+      y = s.pos[((size_t)e * N + lane) * 2 + 1];
+    }
+    const int x_old = x, y_old = y;
+    // reward slot of robot `lane` (r2c): its rank by x + y*W with scanning
+    int slot = lane;
+    if (s.scan) {
+      const int sc = x + y * W;
+      int rank = 0;
+      for (int j = 0; j < N; ++j) rank += __shfl(sc, j) < sc;
+      slot = rank;
+    }
+    const int u = me ? (int)actions[(size_t)e * N + slot] : 255;
+    int tx = x, ty = y;
+    if (u == 0) tx = x - 1;
+    else if (u == 1) tx = x + 1;
+    else if (u == 2) ty = y + 1;
+    else if (u == 3) ty = y - 1;
+    const bool gfree = me && tx >= 0 && tx < W && ty >= 0 && ty < L && !bit_at(gneg, RW, tx, ty);
+    // pre-move distance_map[x, y] (:117-118, 139): the dist layer of the last state
+    double dv = 0.0;
+    if (s.dist && gfree && u < 4) dv = (double)s.dist_plane[((size_t)e * W + tx) * L + ty];
+    double v = 0.0;
+    for (int k = 0; k < N; ++k) {  // slot order; robot z = the one with slot k
+      const int z = s.scan ? (__ffsll((unsigned long long)__ballot(me && slot == k)) - 1) : k;
+      const int zu = __shfl(u, z);
+      if (zu >= 4) continue;  // not a move: nothing happens (no penalty)
+      const int zx = __shfl(tx, z), zy = __shfl(ty, z);
+      const int zok = __shfl((int)gfree, z);
+      const bool occ = __ballot(me && x == zx && y == zy) != 0ull;
+      if (lane == z) {
+        if (zok && !occ) {
+          x = zx;
+          y = zy;
+          if (s.dist) v = v + dv;
+        } else {
+          v = v - s.pen;
+        }
+      }
+    }
+    if (me) {
+      s_x[w][lane] = x;
+      s_y[w][lane] = y;
+    }
+    wave_sync();
+
+    // sense (:177-201): robot i's window, raster order; a cell with grid >= 0
+    // is new (+grid) unless covered before this step or by a lower robot's
+    // window, else -free_penalty; grid < 0 marks an observed obstacle.  Phase
+    // A reads only; the map updates follow in phase B.
+    const int n = 2 * r + 1;
+    const int c0 = y - r;
+    const uint32_t vm = mask32(max(0, -c0), min(n, L - c0));
+    int cnt = 0;
+    if (me) {
+      for (int jj = 0; jj < n; ++jj) {
+        const int j = x - r + jj;
+        if (j < 0 || j >= W) continue;
+        const uint32_t fneg = row_field(gneg + (size_t)j * RW, RW, c0) & vm;
+        const uint32_t fpos = row_field(gpos + (size_t)j * RW, RW, c0) & vm;
+        const uint32_t fcov = row_field(cov + (size_t)j * RW, RW, c0) & vm;
+        uint32_t lower = 0;
+        for (int m = 0; m < lane; ++m) {
+          const int xm = s_x[w][m], ym = s_y[w][m];
+          if (abs(j - xm) <= r) lower |= mask32(max(0, ym - r - c0), min(n, ym + r + 1 - c0));
+        }
+        const uint32_t ge0 = vm & ~fneg;
+        const uint32_t nw = ge0 & ~fcov & ~lower;
+        cnt += __popc(nw);
+        for (uint32_t bits = ge0; bits; bits &= bits - 1) {
+          const int b = __ffs(bits) - 1;
+          if ((nw >> b) & 1u) v = v + (((fpos >> b) & 1u) ? 1.0 : 0.0);
+          else v = v - s.fpen;
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every read above is done
+    // phase B: maps (idempotent ORs of the whole window) and state planes
+    const size_t WL = (size_t)W * L;
+    uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
+    if (me) {
+      uint8_t* pl_obst = pl + (size_t)s.P * WL;
+      uint8_t* pl_free = pl + (size_t)(s.P + 1) * WL;
+      for (int jj = 0; jj < n; ++jj) {
+        const int j = x - r + jj;
+        if (j < 0 || j >= W) continue;
+        const uint32_t fneg = row_field(gneg + (size_t)j * RW, RW, c0) & vm;
+        const uint32_t ge0 = vm & ~fneg;
+        or_field(cov + (size_t)j * RW, RW, c0, ge0);
+        or_field(obst + (size_t)j * RW, RW, c0, fneg);
+        for (uint32_t bits = vm; bits; bits &= bits - 1) {
+          const int b = __ffs(bits) - 1;
+          const size_t cell = (size_t)j * L + (c0 + b);
+          if ((fneg >> b) & 1u) pl_obst[cell] = 1;
+          else pl_free[cell] = 0;
+        }
+      }
+    }
+    const bool moved = me && (x != x_old || y != y_old);
+    const size_t lay = (size_t)(s.scan ? 0 : lane) * WL;
+    if (moved) pl[lay + (size_t)x_old * L + y_old] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clears land before the sets
+    if (moved) pl[lay + (size_t)x * L + y] = 1;
+
+    // motion_penalty(a) on every slot (:203-208, 227-243): a is the quotient
+    // left in `action` after the digit loop; a == inv(a) never holds
+    const int q = quot ? quot[e] : 0;
+    const int ap = s.a_prev[e];
+    if ((q < 0 || q >= 4) && lane == 0) atomicOr(s.err, ERR_KEY);
+    v = v + ((q == ap) ? 0.0 : -1.0);
+    if (me) {
+      s_v[w][slot] = v;
+      s.pos[((size_t)e * N + lane) * 2] = x;
+      s.pos[((size_t)e * N + lane) * 2 + 1] = y;
+    }
+    cnt = wave_sum(cnt);
+    wave_sync();
+    int dn = 0;
+    if (lane == 0) {
+      double total = np_pairwise_sum(s_v[w], N);
+      const int cs = s.currstep[e] + 1;
+      const uint32_t cc = s.cov_cnt[e] + (uint32_t)cnt;
+      const double pc = (double)cc / (double)s.numpos[g];
+      const double dt = s.done_thresh[e];
+      const bool cond = (dt < 1.0 ? dt : 1.0) <= pc;  // min(_done_thresh, 1) <= percent_covered()
+      if (cond) total = total + s.term;
+      if (cond) s.done_thresh[e] = dt + s.dincr;  // done() (:408-411)
+      dn = cond || (s.maxsteps > 0 && cs == s.maxsteps);
+      s.a_prev[e] = q;
+      s.currstep[e] = cs;
+      s.cov_cnt[e] = cc;
+      reward[e] = total;
+      done[e] = (uint8_t)dn;
+    }
+    is_done = __shfl(dn, 0) != 0;
+  }
+  if (is_done && s.auto_reset) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the step's map ORs land first
+    sg_reset_env(s, e, lane, nullptr);
+  }
+}
+
+// --------------------------------------------------------------------------
+// get_state (:305-317) planes: full rewrite of the uint8 layers (after a
+// reset / state upload) and the distance layer of every env.
+// --------------------------------------------------------------------------
+template <bool kLds>
+__global__ __launch_bounds__(256) void sg_dist_kernel(SState s, int pitch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_px[kMaxAgents], s_py[kMaxAgents];
+  __shared__ int s_max;
+  const int e = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
+  const int W = s.W, L = s.L, RW = s.RW, N = s.N;
+  const size_t mw = (size_t)W * RW, WL = (size_t)W * L;
+  const uint64_t* cov = s.cov + (size_t)e * mw;
+  uint16_t* H = kLds ? reinterpret_cast<uint16_t*>(smem) : s.scratch + (size_t)e * W * pitch;
+  if (tid == 0) s_max = 0;
+
+  if (s.full[e]) {  // uniform: rewrite every uint8 layer
+    if (tid < N) {
+      s_px[tid] = s.pos[((size_t)e * N + tid) * 2];
+      s_py[tid] = s.pos[((size_t)e * N + tid) * 2 + 1];
+    }
+    uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
+    const uint64_t* ob = s.obst + (size_t)e * mw;
+    for (size_t i = tid; i < WL; i += NT) {
+      const int u = div_L(s, (int)i), v = (int)i - u * L;
+      const size_t wi = (size_t)u * RW + (v >> 6);
+      const int b = v & 63;
+      for (int p = 0; p < s.P; ++p) pl[(size_t)p * WL + i] = 0;
+      pl[(size_t)s.P * WL + i] = (uint8_t)((ob[wi] >> b) & 1ull);
+      pl[(size_t)(s.P + 1) * WL + i] = (uint8_t)(((cov[wi] >> b) & 1ull) ^ 1ull);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < N) pl[(size_t)(s.scan ? 0 : tid) * WL + (size_t)s_px[tid] * L + s_py[tid]] = 1;
+    if (tid == 0) s.full[e] = 0;
+  }
+
+  // row pass: H[u][v] = distance along row u to the nearest source (_free != 0)
+  for (int u = tid; u < W; u += NT) {
+    const uint64_t* row = cov + (size_t)u * RW;
+    uint16_t* h = H + (size_t)u * pitch;
+    int last = -(1 << 20);
+    for (int wv = 0; wv < RW; ++wv) {
+      const int nb = min(64, L - wv * 64);
+      const uint64_t src = ~row[wv] & low_mask(nb);
+      if (src == low_mask(nb)) {  // no sensed cell in this word
+        for (int b = 0; b < nb; ++b) h[wv * 64 + b] = 0;
+        last = wv * 64 + nb - 1;
+        continue;
+      }
+      for (int b = 0; b < nb; ++b) {
+        const int v = wv * 64 + b;
+        if ((src >> b) & 1ull) last = v;
+        h[v] = (uint16_t)min(v - last, kInfD);
+      }
+    }
+    int next = 1 << 21;
+    for (int wv = RW - 1; wv >= 0; --wv) {
+      const int nb = min(64, L - wv * 64);
+      const uint64_t src = ~row[wv] & low_mask(nb);
+      if (src == low_mask(nb)) {
+        next = wv * 64;
+        continue;
+      }
+      for (int b = nb - 1; b >= 0; --b) {
+        const int v = wv * 64 + b;
+        if ((src >> b) & 1ull) next = v;
+        const int hv = h[v];
+        if (next - v < hv) h[v] = (uint16_t)(next - v);
+      }
+    }
+  }
+  __syncthreads();
+  // column pass: d(u, v) = min_u' |u - u'| + H[u'][v], down then up
+  int mx = 0;
+  for (int v = tid; v < L; v += NT) {
+    int f = 1 << 20;
+    for (int u = 0; u < W; ++u) {
+      f = min(f + 1, (int)H[(size_t)u * pitch + v]);
+      H[(size_t)u * pitch + v] = (uint16_t)min(f, kInfD);
+    }
+    f = 1 << 20;
+    for (int u = W - 1; u >= 0; --u) {
+      f = min(f + 1, (int)H[(size_t)u * pitch + v]);
+      H[(size_t)u * pitch + v] = (uint16_t)min(f, kInfD);
+      mx = max(mx, min(f, kInfD));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  if ((tid & 63) == 0) atomicMax(&s_max, mx);
+  __syncthreads();
+  const int M = s_max;
+  float* out = s.dist_plane + (size_t)e * WL;
+  if (M >= kInfD) {  // no source cell: SciPy's -1 everywhere -> 1 - (-1)
+    for (size_t i = tid; i < WL; i += NT) out[i] = 2.0f;
+    return;
+  }
+  const float Mf = (float)M;
+  for (size_t i = tid; i < WL; i += NT) {
+    const int u = div_L(s, (int)i), v = (int)i - u * L;
+    out[i] = dist_value((float)H[(size_t)u * pitch + v], Mf);
+  }
+}
+
+// --------------------------------------------------------------------------
+// grid pool: int8 [G][W][L] -> bit rows, numpos; Bernoulli generation
+// --------------------------------------------------------------------------
+__global__ void sg_pack_kernel(SState s, const int8_t* __restrict__ grids, uint64_t* gneg,
+                               uint64_t* gpos, int32_t* numpos) {
+  const size_t total = (size_t)s.G * s.W * s.RW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int wv = (int)(i % s.RW);
+    const size_t gx = i / s.RW;
+    const int x = (int)(gx % s.W), g = (int)(gx / s.W);
+    const int8_t* src = grids + ((size_t)g * s.W + x) * s.L;
+    uint64_t neg = 0, pos = 0;
+    for (int b = 0; b < 64 && wv * 64 + b < s.L; ++b) {
+      const int8_t c = src[wv * 64 + b];
+      neg |= (uint64_t)(c < 0) << b;
+      pos |= (uint64_t)(c > 0) << b;
+    }
+    gneg[i] = neg;
+    gpos[i] = pos;
+    if (pos) atomicAdd(&numpos[g], __popcll(pos));
+  }
+}
+
+__global__ void sg_gen_kernel(SState s, uint64_t seed, uint32_t thresh, uint64_t* gneg, uint64_t* gpos,
+                              int32_t* numpos) {
+  const size_t total = (size_t)s.G * s.W * s.RW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int wv = (int)(i % s.RW);
+    const size_t gx = i / s.RW;
+    const int x = (int)(gx % s.W), g = (int)(gx / s.W);
+    const int nb = min(64, s.L - wv * 64);
+    uint64_t neg = 0;
+    for (int q = 0; q < 16; ++q) {
+      const uint4 r = philox(seed, make_uint4((uint32_t)x, (uint32_t)wv, (uint32_t)g, 0x5367656eu + ((uint32_t)q << 28)));
+      neg |= (uint64_t)(r.x < thresh) << (4 * q);
+      neg |= (uint64_t)(r.y < thresh) << (4 * q + 1);
+      neg |= (uint64_t)(r.z < thresh) << (4 * q + 2);
+      neg |= (uint64_t)(r.w < thresh) << (4 * q + 3);
+    }
+    neg &= low_mask(nb);
+    const uint64_t pos = ~neg & low_mask(nb);
+    gneg[i] = neg;
+    gpos[i] = pos;
+    if (pos) atomicAdd(&numpos[g], __popcll(pos));
+  }
+}
+
+}  // namespace mcs
+
+// ==========================================================================
+// C ABI
+// ==========================================================================
+namespace {
+
+int sg_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int sg_fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  mc::set_last_error(buf);
+  return code;
+}
+
+#define SG_TRY(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess) return sg_fail(MC_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+struct SgEnv {
+  mc_sg_config cfg;
+  mcs::SState s;
+  mc_sg_layout lay;
+  int device = 0;
+  int pitch = 0;      // u16 elements per distance-plane row
+  bool lds = true;    // distance planes in LDS (else s.scratch)
+  int dist_nt = 256;
+  bool grids_set = false;
+  bool stale = true;  // the dist layer does not describe the current maps
+  std::vector<void*> allocs;
+};
+
+SgEnv* as_sg(void* p) { return static_cast<SgEnv*>(p); }
+
+int sg_alloc(SgEnv* E, void** p, size_t bytes) {
+  void* q = nullptr;
+  SG_TRY(hipMalloc(&q, bytes < 16 ? 16 : bytes));
+  SG_TRY(hipMemset(q, 0, bytes < 16 ? 16 : bytes));
+  E->allocs.push_back(q);
+  E->lay.state_bytes += (int64_t)bytes;
+  *p = q;
+  return MC_OK;
+}
+
+struct SgField {
+  void* ptr;
+  int64_t bytes;
+};
+
+SgField sg_field(SgEnv* E, int f) {
+  const mcs::SState& s = E->s;
+  const int64_t B = s.B, N = s.N, G = s.G, mw = (int64_t)s.W * s.RW;
+  switch (f) {
+    case MC_SG_FIELD_POS: return {s.pos, B * N * 8};
+    case MC_SG_FIELD_COVERED: return {s.cov, B * mw * 8};
+    case MC_SG_FIELD_OBST: return {s.obst, B * mw * 8};
+    case MC_SG_FIELD_COV_COUNT: return {s.cov_cnt, B * 4};
+    case MC_SG_FIELD_CURRSTEP: return {s.currstep, B * 4};
+    case MC_SG_FIELD_DONE_THRESH: return {s.done_thresh, B * 8};
+    case MC_SG_FIELD_A_PREV: return {s.a_prev, B * 4};
+    case MC_SG_FIELD_ENV_GRID: return {s.env_grid, B * 4};
+    case MC_SG_FIELD_EPISODE: return {s.episode, B * 4};
+    case MC_SG_FIELD_NUMPOS: return {(void*)s.numpos, G * 4};
+    case MC_SG_FIELD_GRID_NEG: return {(void*)s.gneg, G * mw * 8};
+    case MC_SG_FIELD_GRID_POS: return {(void*)s.gpos, G * mw * 8};
+    default: return {nullptr, -1};
+  }
+}
+
+int sg_ready(SgEnv* E, const char* who) {
+  if (!E->grids_set) return sg_fail(MC_ESTATE, "%s: grids not set (mc_sg_set_grids / mc_sg_generate_grids)", who);
+  if (!E->s.planes || !E->s.dist_plane) return sg_fail(MC_ESTATE, "%s: state buffers not registered (mc_sg_set_obs)", who);
+  return MC_OK;
+}
+
+hipError_t launch_dist(SgEnv* E, hipStream_t st) {
+  const size_t lds = E->lds ? (size_t)E->s.W * E->pitch * 2 : 0;
+  if (E->lds)
+    hipLaunchKernelGGL(mcs::sg_dist_kernel<true>, dim3(E->s.B), dim3(E->dist_nt), lds, st, E->s, E->pitch);
+  else
+    hipLaunchKernelGGL(mcs::sg_dist_kernel<false>, dim3(E->s.B), dim3(E->dist_nt), 0, st, E->s, E->pitch);
+  return hipGetLastError();
+}
+
+int check_numpos(SgEnv* E, hipStream_t st) {
+  std::vector<int32_t> np(E->s.G);
+  SG_TRY(hipMemcpyAsync(np.data(), E->s.numpos, np.size() * 4, hipMemcpyDeviceToHost, st));
+  SG_TRY(hipStreamSynchronize(st));
+  for (int g = 0; g < E->s.G; ++g)
+    if (np[g] <= 0)
+      return sg_fail(MC_EINVAL,
+                     "grid %d has no cell > 0: percent_covered() divides by count_nonzero(grid > 0) "
+                     "(super_grid_rl.py:420-421)",
+                     g);
+  E->grids_set = true;
+  return MC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
+  if (!cfg || !out_env) return sg_fail(MC_EINVAL, "mc_sg_create: null argument");
+  const mc_sg_config& c = *cfg;
+  if (c.num_envs < 1) return sg_fail(MC_EINVAL, "num_envs must be >= 1");
+  if (c.num_agents < 1 || c.num_agents > mcs::kMaxAgents) return sg_fail(MC_EINVAL, "numrobot must be in [1, 64]");
+  if (c.width < 1 || c.length < 1 || c.width > mcs::kMaxSide || c.length > mcs::kMaxSide)
+    return sg_fail(MC_EINVAL, "grid sides must be in [1, %d]", mcs::kMaxSide);
+  if ((int64_t)c.width * c.length < c.num_agents) return sg_fail(MC_EINVAL, "more robots than cells");
+  if (c.num_grids < 1) return sg_fail(MC_EINVAL, "num_grids must be >= 1");
+  if (c.senseradius < 0 || c.senseradius > mcs::kMaxRadius) return sg_fail(MC_EINVAL, "senseradius must be in [0, 15]");
+  SG_TRY(hipSetDevice(hip_device));
+  SgEnv* E = new SgEnv();
+  E->cfg = c;
+  E->device = hip_device;
+  E->lay = mc_sg_layout{};
+  mcs::SState& s = E->s;
+  s = mcs::SState{};
+  s.B = c.num_envs;
+  s.N = c.num_agents;
+  s.W = c.width;
+  s.L = c.length;
+  s.G = c.num_grids;
+  s.RW = (c.length + 63) / 64;
+  s.r = c.senseradius;
+  s.P = c.use_scanning ? 1 : c.num_agents;
+  s.pen = c.collision_penalty;
+  s.fpen = c.free_penalty;
+  s.term = c.terminal_reward;
+  s.dincr = c.done_incr;
+  s.dist = c.dist_reward != 0;
+  s.scan = c.use_scanning != 0;
+  s.maxsteps = c.maxsteps;
+  s.auto_reset = c.auto_reset != 0;
+  s.grid_mode = c.reset_grid_mode;
+  s.mg_L = mc::magic_div((uint32_t)c.length);
+  s.seed = c.seed;
+  // distance planes: u16 rows with an odd dword pitch (the row pass writes
+  // column v of W rows at once: distinct banks)
+  E->pitch = ((c.length + 1) / 2) * 2;
+  if (((E->pitch / 2) & 1) == 0) E->pitch += 2;
+  E->lds = (size_t)c.width * E->pitch * 2 <= mcs::kLdsLimit;
+  const int side = c.width > c.length ? c.width : c.length;
+  E->dist_nt = side <= 64 ? 64 : (side <= 128 ? 128 : 256);
+  const size_t B = s.B, N = s.N, G = s.G, mw = (size_t)s.W * s.RW;
+  void* p;
+  int rc = 0;
+#define SG_ALLOC(field, type, bytes)        \
+  rc = sg_alloc(E, &p, (bytes));            \
+  if (rc) { mc_sg_destroy(E); return rc; }  \
+  s.field = (type)p;
+  SG_ALLOC(gneg, const uint64_t*, G * mw * 8);
+  SG_ALLOC(gpos, const uint64_t*, G * mw * 8);
+  SG_ALLOC(numpos, const int32_t*, G * 4);
+  SG_ALLOC(env_grid, int32_t*, B * 4);
+  SG_ALLOC(pos, int32_t*, B * N * 8);
+  SG_ALLOC(cov, uint64_t*, B * mw * 8);
+  SG_ALLOC(obst, uint64_t*, B * mw * 8);
+  SG_ALLOC(cov_cnt, uint32_t*, B * 4);
+  SG_ALLOC(currstep, int32_t*, B * 4);
+  SG_ALLOC(done_thresh, double*, B * 8);
+  SG_ALLOC(a_prev, int32_t*, B * 4);
+  SG_ALLOC(episode, uint32_t*, B * 4);
+  SG_ALLOC(full, uint8_t*, B);
+  SG_ALLOC(err, uint32_t*, 4);
+  if (!E->lds) {
+    SG_ALLOC(scratch, uint16_t*, B * s.W * E->pitch * 2);
+  }
+#undef SG_ALLOC
+  {
+    std::vector<int32_t> eg(B), ap(B, -1);
+    std::vector<double> dt(B, c.done_thresh);
+    std::vector<uint8_t> fl(B, 1);
+    for (size_t e = 0; e < B; ++e) eg[e] = (int32_t)(e % G);
+    hipError_t he = hipMemcpy(s.env_grid, eg.data(), B * 4, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(s.a_prev, ap.data(), B * 4, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(s.done_thresh, dt.data(), B * 8, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(s.full, fl.data(), B, hipMemcpyHostToDevice);
+    if (he != hipSuccess) {
+      mc_sg_destroy(E);
+      return sg_fail(MC_EHIP, "mc_sg_create: %s", hipGetErrorString(he));
+    }
+  }
+  E->lay.pos_layers = s.P;
+  E->lay.obs_layers = s.P + 2;
+  E->lay.row_words = s.RW;
+  *out_env = E;
+  return MC_OK;
+}
+
+void mc_sg_destroy(void* env) {
+  SgEnv* E = as_sg(env);
+  if (!E) return;
+  (void)hipSetDevice(E->device);
+  for (void* p : E->allocs) (void)hipFree(p);
+  delete E;
+}
+
+int mc_sg_query(void* env, mc_sg_layout* out) {
+  SgEnv* E = as_sg(env);
+  if (!E || !out) return sg_fail(MC_EINVAL, "mc_sg_query: null argument");
+  *out = E->lay;
+  return MC_OK;
+}
+
+int mc_sg_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_grids) return sg_fail(MC_EINVAL, "mc_sg_set_grids: null argument");
+  if (num_grids != E->s.G) return sg_fail(MC_EINVAL, "mc_sg_set_grids: %d grids, config says %d", num_grids, E->s.G);
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemsetAsync((void*)E->s.numpos, 0, (size_t)E->s.G * 4, st));
+  const size_t total = (size_t)E->s.G * E->s.W * E->s.RW;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(mcs::sg_pack_kernel, dim3(blocks), dim3(256), 0, st, E->s, dev_grids,
+                     (uint64_t*)E->s.gneg, (uint64_t*)E->s.gpos, (int32_t*)E->s.numpos);
+  SG_TRY(hipGetLastError());
+  E->stale = true;
+  return check_numpos(E, st);
+}
+
+int mc_sg_generate_grids(void* env, uint64_t seed, double p_obst, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E) return sg_fail(MC_EINVAL, "mc_sg_generate_grids: null env");
+  if (!(p_obst >= 0.0 && p_obst < 1.0)) return sg_fail(MC_EINVAL, "p_obst must be in [0, 1)");
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemsetAsync((void*)E->s.numpos, 0, (size_t)E->s.G * 4, st));
+  const size_t total = (size_t)E->s.G * E->s.W * E->s.RW;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  const uint32_t thresh = (uint32_t)(p_obst * 4294967296.0);
+  hipLaunchKernelGGL(mcs::sg_gen_kernel, dim3(blocks), dim3(256), 0, st, E->s, seed, thresh,
+                     (uint64_t*)E->s.gneg, (uint64_t*)E->s.gpos, (int32_t*)E->s.numpos);
+  SG_TRY(hipGetLastError());
+  E->stale = true;
+  return check_numpos(E, st);
+}
+
+int mc_sg_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_env_grid) return sg_fail(MC_EINVAL, "mc_sg_set_env_grids: null argument");
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemcpyAsync(E->s.env_grid, dev_env_grid, (size_t)E->s.B * 4, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  E->stale = true;
+  return MC_OK;
+}
+
+int mc_sg_set_obs(void* env, uint8_t* dev_planes, float* dev_dist) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_planes || !dev_dist) return sg_fail(MC_EINVAL, "mc_sg_set_obs: null argument");
+  E->s.planes = dev_planes;
+  E->s.dist_plane = dev_dist;
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemset(E->s.full, 1, (size_t)E->s.B));
+  E->stale = true;
+  return MC_OK;
+}
+
+int mc_sg_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E) return sg_fail(MC_EINVAL, "mc_sg_reset: null env");
+  int rc = sg_ready(E, "mc_sg_reset");
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  const int blocks = (E->s.B + mcs::kEnvsPerBlock - 1) / mcs::kEnvsPerBlock;
+  hipLaunchKernelGGL(mcs::sg_reset_kernel, dim3(blocks), dim3(64 * mcs::kEnvsPerBlock), 0, st, E->s,
+                     dev_env_mask, dev_pos);
+  SG_TRY(hipGetLastError());
+  SG_TRY(launch_dist(E, st));
+  E->stale = false;
+  return MC_OK;
+}
+
+int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, double* dev_reward,
+               uint8_t* dev_done, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_actions || !dev_reward || !dev_done) return sg_fail(MC_EINVAL, "mc_sg_step: null argument");
+  int rc = sg_ready(E, "mc_sg_step");
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  if (E->stale) SG_TRY(launch_dist(E, st));  // the pre-move distance_map of the current maps
+  const int blocks = (E->s.B + mcs::kEnvsPerBlock - 1) / mcs::kEnvsPerBlock;
+  hipLaunchKernelGGL(mcs::sg_step_kernel, dim3(blocks), dim3(64 * mcs::kEnvsPerBlock), 0, st, E->s,
+                     dev_actions, dev_quot, dev_reward, dev_done);
+  SG_TRY(hipGetLastError());
+  SG_TRY(launch_dist(E, st));
+  E->stale = false;
+  return MC_OK;
+}
+
+int64_t mc_sg_field_bytes(void* env, int32_t f) {
+  SgEnv* E = as_sg(env);
+  if (!E) return sg_fail(MC_EINVAL, "mc_sg_field_bytes: null env");
+  SgField d = sg_field(E, f);
+  if (!d.ptr) return sg_fail(MC_EINVAL, "unknown state field %d", f);
+  return d.bytes;
+}
+
+int mc_sg_get_state(void* env, int32_t f, void* dev_dst, int64_t bytes, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_dst) return sg_fail(MC_EINVAL, "mc_sg_get_state: null argument");
+  SgField d = sg_field(E, f);
+  if (!d.ptr) return sg_fail(MC_EINVAL, "unknown state field %d", f);
+  if (bytes != d.bytes) return sg_fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemcpyAsync(dev_dst, d.ptr, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MC_OK;
+}
+
+int mc_sg_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E || !dev_src) return sg_fail(MC_EINVAL, "mc_sg_set_state: null argument");
+  SgField d = sg_field(E, f);
+  if (!d.ptr) return sg_fail(MC_EINVAL, "unknown state field %d", f);
+  if (bytes != d.bytes) return sg_fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  SG_TRY(hipMemcpyAsync(d.ptr, dev_src, (size_t)bytes, hipMemcpyDeviceToDevice, st));
+  if (f == MC_SG_FIELD_GRID_NEG || f == MC_SG_FIELD_GRID_POS || f == MC_SG_FIELD_NUMPOS) E->grids_set = true;
+  SG_TRY(hipMemsetAsync(E->s.full, 1, (size_t)E->s.B, st));
+  E->stale = true;
+  return MC_OK;
+}
+
+int mc_sg_check(void* env, void* stream) {
+  SgEnv* E = as_sg(env);
+  if (!E) return sg_fail(MC_EINVAL, "mc_sg_check: null env");
+  hipStream_t st = (hipStream_t)stream;
+  SG_TRY(hipSetDevice(E->device));
+  uint32_t err = 0;
+  SG_TRY(hipMemcpyAsync(&err, E->s.err, 4, hipMemcpyDeviceToHost, st));
+  SG_TRY(hipStreamSynchronize(st));
+  if (err) {
+    SG_TRY(hipMemsetAsync(E->s.err, 0, 4, st));
+    SG_TRY(hipStreamSynchronize(st));
+    return sg_fail(MC_EDEVICE, "device error word 0x%x (4=placement 8=inject 16=motion_penalty KeyError)", err);
+  }
+  return MC_OK;
+}
+
+}  // extern "C"

@@ -44,6 +44,8 @@ def test_struct_layout_and_version(lib):
     assert lib.mc_abi_version() == _lib.ABI_VERSION
     assert lib.mc_struct_size(0) == ctypes.sizeof(_lib.McConfig)
     assert lib.mc_struct_size(1) == ctypes.sizeof(_lib.McLayout)
+    assert lib.mc_struct_size(2) == ctypes.sizeof(_lib.McSgConfig)
+    assert lib.mc_struct_size(3) == ctypes.sizeof(_lib.McSgLayout)
     assert lib.mc_struct_size(7) == -1
 
 
@@ -164,3 +166,47 @@ def test_tile_block_layout_round_trip():
         bit = (int(grid[1, 2, ti, tj]) >> (8 * r + c)) & 1
         x, y = 8 * ti + r, 8 * tj + c
         assert bit == (cells[1, 2, x, y] if x < 130 and y < 70 else 0)
+
+
+def test_super_action_decode_reference_semantics():
+    """super_grid_rl.py:88-98,203-208: base-4 digits slot 0 first, the quotient
+    is what motion_penalty sees (KeyError unless 0 <= q < 4), -1/None sentinel."""
+    from marlcov.super_env import decode_super_action
+    assert decode_super_action(None, 2) is None
+    assert decode_super_action(-1, 3) is None
+    d, q = decode_super_action(4 * 3 + 2, 2)
+    assert d.tolist() == [2, 3] and q == 0
+    d, q = decode_super_action(3 * 16 + 7, 2)
+    assert d.tolist() == [3, 1] and q == 3
+    with pytest.raises(KeyError):
+        decode_super_action(4 * 16, 2)
+    with pytest.raises(KeyError):
+        decode_super_action(-2, 1)
+    d, q = decode_super_action(np.int64(9), 2)
+    assert d.tolist() == [1, 2] and q == 0
+    d, q = decode_super_action([1, 7, 3], 3)
+    assert d.tolist() == [1, 4, 3] and q == 0
+
+
+def test_super_row_bitboards_round_trip():
+    from marlcov.super_env import pack_rows, unpack_rows
+    rs = np.random.RandomState(0)
+    for shape in [(3, 1), (5, 63), (4, 64), (7, 65), (2, 130)]:
+        c = (rs.rand(2, *shape) < 0.4).astype(np.uint8)
+        w = pack_rows(c)
+        assert w.shape == (2, shape[0], (shape[1] + 63) // 64)
+        np.testing.assert_array_equal(unpack_rows(w, shape[1]), c)
+        # bit (y & 63) of word y >> 6 is cell y (include/marlcov.h)
+        x, y = 1, shape[1] - 1
+        assert ((int(w[0, x, y >> 6]) >> (y & 63)) & 1) == c[0, x, y]
+
+
+def test_super_create_rejects_bad_config(lib):
+    from marlcov import _lib
+    c = _lib.McSgConfig(num_envs=1, num_agents=2, width=8, length=8, num_grids=1, senseradius=1)
+    h = ctypes.c_void_p()
+    for field, bad in (("num_agents", 65), ("senseradius", 16), ("width", 0), ("num_envs", 0)):
+        cc = _lib.McSgConfig.from_buffer_copy(c)
+        setattr(cc, field, bad)
+        assert lib.mc_sg_create(ctypes.byref(cc), 0, ctypes.byref(h)) == _lib.MC_EINVAL
+        assert lib.mc_last_error()
