@@ -45,7 +45,30 @@ CONFIGS = {
     "c2_dijkstra": dict(numrobot=4, width=128, sensor_config={"num_lasers": 21, "range": 10}, envs=4096,
                         extra={"dijkstra_input": 1},
                         desc="C2 + dijkstra_input obs layer (4 layers)"),
+    # the centralized SuperGridRL on C2's shape (full-map
+    # state every step: P+2 uint8 layers + float32 distance layer); not a
+    # BASELINE metric config
+    "sg_c2": dict(env="super", numrobot=4, width=128, envs=4096, sensor_config={"range": 0},
+                  sg=dict(senseradius=2, free_penalty=0.2, dist_reward=1, use_scanning=0),
+                  desc="SuperGridRL: 4 agents, 128x128 grid p_obst=0.1, senseradius 2, free_penalty 0.2, "
+                       "dist_reward, full-map state (4 position + obstacle + free uint8 layers, "
+                       "float32 distance layer), episode cut 1000"),
 }
+
+SG_BASE = dict(train_maxsteps=1000, test_maxsteps=1000, collision_penalty=5, done_thresh=1, done_incr=0,
+               terminal_reward=30)
+
+
+def sg_algorithmic_bytes_per_env_step(n_agents, r, W, L):
+    """SuperGridRL: per env the float32 distance layer write
+    (4 B per cell) and the read of the covered bit map its transform needs
+    (W * ceil(L/64) * 8 B); per agent the window bits of grid / covered /
+    obstacle read (3 * ceil(s^2/8)), covered / obstacle ORs (2 * ceil(s^2/8)),
+    the obstacle / free layer bytes of the window (2 * s^2), two position-layer
+    bytes, 1 B action and 8 B position r/w (s = 2r+1); per env 32 B."""
+    s2 = (2 * r + 1) ** 2
+    bits = math.ceil(s2 / 8)
+    return W * L * 4 + W * math.ceil(L / 64) * 8 + n_agents * (5 * bits + 2 * s2 + 2 + 1 + 8) + 32
 
 
 def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3, full_map_cells=0):
@@ -72,6 +95,8 @@ def _cpu_worker(args):
     from oracle.cpu_ref import DecGridRLRef
 
     c = CONFIGS[cfgname]
+    if c.get("env") == "super":
+        return _cpu_worker_super(seed, secs, c)
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"],
                allow_even_beams=True, **c.get("extra", {}))
     rs = np.random.RandomState(1000 + seed)
@@ -85,6 +110,29 @@ def _cpu_worker(args):
         _, _, done = env.step(acts[n % 4096])
         n += 1
         if done:
+            env.reset(False, None)
+        if n % 8 == 0 and time.perf_counter() - t0 >= secs:
+            break
+    return n, time.perf_counter() - t0
+
+
+def _cpu_worker_super(seed, secs, c):
+    import numpy as np
+    from oracle.super_ref import SuperGridRLRef
+
+    cfg = dict(SG_BASE, numrobot=c["numrobot"], **c["sg"])
+    rs = np.random.RandomState(1000 + seed)
+    grid = rs.choice([1.0, -1.0], size=(c["width"], c["width"]), p=[0.9, 0.1])
+    np.random.seed(seed)
+    env = SuperGridRLRef([grid], cfg)
+    N = c["numrobot"]
+    acts = rs.randint(0, 4 ** N, size=4096)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        _, _, done = env.step(int(acts[n % 4096]))
+        n += 1
+        if done or env._currstep == cfg["train_maxsteps"]:  # the episode cut of Utils/utils.py:25-28
             env.reset(False, None)
         if n % 8 == 0 and time.perf_counter() - t0 >= secs:
             break
@@ -107,10 +155,12 @@ def cpu_baseline(cfgname, procs, secs):
                     break
     except OSError:
         pass
+    port = ("oracle/super_ref.py (SuperGridRL step restated, per-cell Python sense loop kept)"
+            if CONFIGS[cfgname].get("env") == "super" else
+            "oracle/cpu_ref.py (reference step restated, per-cell Python beam march kept)")
     return {"value": round(rate, 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
             "sample": f"{procs} processes x {secs:.1f} s, one env each, {CONFIGS[cfgname]['desc']}, "
-                      f"random joint actions; oracle/cpu_ref.py (reference step restated, "
-                      f"per-cell Python beam march kept); host CPU: {cpu}"}
+                      f"random joint actions; {port}; host CPU: {cpu}"}
 
 
 def load_traffic(cfgname):
@@ -162,6 +212,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if c.get("env") == "super":
+        return bench_super(args, c, B, cpu, world, rank, dev)
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
                maxsteps=args.maxsteps, **c.get("extra", {}))
     dj = bool(cfg.get("dijkstra_input"))
@@ -278,6 +330,105 @@ def main():
                      "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),
                      "kernel_us_from": "per-launch HIP events" if args.eager else
                                        "HIP events around the replayed launches / K (includes kernel boundaries)",
+                     "alg_bytes_per_env_step": bpe},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def timed_launches(step_fn, dev, K, eager):
+    """Replay K launches (hipGraph chunks unless eager) between barrier +
+    synchronize; returns (elapsed s, ms per launch from HIP events on the
+    launch stream)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    stream = torch.cuda.current_stream(dev)
+    graphs = []
+    if not eager:
+        chunk = max(1, min(100, K))
+        for c0 in range(0, K, chunk):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                cs = torch.cuda.current_stream(dev).cuda_stream
+                for i in range(c0, min(K, c0 + chunk)):
+                    step_fn(i, cs)
+            graphs.append(g)
+        torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    if eager:
+        for i in range(K):
+            step_fn(i, stream.cuda_stream)
+    else:
+        for g in graphs:
+            g.replay()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    return t1 - t0, ev0.elapsed_time(ev1) / K
+
+
+def bench_super(args, c, B, cpu, world, rank, dev):
+    """SuperGridRL workload: one step = sg_step_kernel +
+    sg_dist_kernel over every env of this GPU's shard."""
+    import torch
+    import torch.distributed as dist
+
+    import marlcov
+    from marlcov.shards import aggregate_rate, rank_seeds, reduce_run
+
+    N, W = c["numrobot"], c["width"]
+    cfg = dict(SG_BASE, numrobot=N, **c["sg"])
+    seeds = rank_seeds(rank)
+    env = marlcov.BatchSuperGridEnv(cfg, B, gen=dict(width=W, length=W, prob_obst=0.1, seed=seeds["grid_seed"],
+                                                     num_grids=B),
+                                    device=dev, seed=seeds["env_seed"], auto_reset=True, maxsteps=args.maxsteps)
+    env.reset()
+    K, Wm = args.steps, args.warmup
+    g = torch.Generator(device=dev)
+    g.manual_seed(seeds["action_seed"])
+    actions = torch.randint(0, 4, (Wm + K, B, N), dtype=torch.uint8, device=dev, generator=g)
+    rp, dp = env.reward.data_ptr(), env.done.data_ptr()
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    for i in range(Wm):
+        assert env.step_raw(actions[i].data_ptr(), rp, dp, sp) == 0, env.lib.mc_last_error()
+    torch.cuda.synchronize(dev)
+    env.check()
+    elapsed, step_ms = timed_launches(lambda i, st: env.step_raw(actions[Wm + i].data_ptr(), rp, dp, st),
+                                      dev, K, args.eager)
+    env.check()
+    stats = torch.stack([env.reward.sum(), env.done.to(torch.float64).sum()])
+    stats, elapsed = reduce_run(stats, elapsed, world)
+    value = aggregate_rate(B, world, K, elapsed)
+    bpe = sg_algorithmic_bytes_per_env_step(N, cfg["senseradius"], W, W)
+    achieved = bpe * B / (step_ms * 1e-3) / 1e9
+    line = {
+        "metric": "env-steps/sec (whole node), SuperGridRL 4-agent 128x128 (SURVEY 8(f) rank 2; not the "
+                  "BASELINE metric)",
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": Wm,
+        "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64+u64+f32",
+        "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
+        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * world,
+                   "launch": "eager" if args.eager else "hipGraph replay", "parallelism": f"env-shard x{world}",
+                   "auto_reset": True, "maxsteps": args.maxsteps},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic(args.config),
+                     "kernel": "mcs::sg_step_kernel + mcs::sg_dist_kernel (one step)",
+                     "kernel_us": round(step_ms * 1e3, 3),
+                     "kernel_us_from": "HIP events around the launches / K (both kernels of a step)",
                      "alg_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }

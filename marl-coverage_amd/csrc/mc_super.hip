@@ -32,6 +32,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <string>
 #include <vector>
@@ -398,38 +399,140 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
 // get_state (:305-317) planes: full rewrite of the uint8 layers (after a
 // reset / state upload) and the distance layer of every env.
 // --------------------------------------------------------------------------
+// full rewrite of env e's uint8 layers (after a reset / state upload); the
+// caller reads s.full[e] first (uniform) and this clears it
+__device__ void write_full_layers(const SState& s, int e, int tid, int NT, int* s_px, int* s_py) {
+  const int W = s.W, L = s.L, RW = s.RW, N = s.N;
+  const size_t mw = (size_t)W * RW, WL = (size_t)W * L;
+  const uint64_t* cov = s.cov + (size_t)e * mw;
+  if (tid < N) {
+    s_px[tid] = s.pos[((size_t)e * N + tid) * 2];
+    s_py[tid] = s.pos[((size_t)e * N + tid) * 2 + 1];
+  }
+  uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
+  const uint64_t* ob = s.obst + (size_t)e * mw;
+  for (size_t i = tid; i < WL; i += NT) {
+    const int u = div_L(s, (int)i), v = (int)i - u * L;
+    const size_t wi = (size_t)u * RW + (v >> 6);
+    const int b = v & 63;
+    for (int p = 0; p < s.P; ++p) pl[(size_t)p * WL + i] = 0;
+    pl[(size_t)s.P * WL + i] = (uint8_t)((ob[wi] >> b) & 1ull);
+    pl[(size_t)(s.P + 1) * WL + i] = (uint8_t)(((cov[wi] >> b) & 1ull) ^ 1ull);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < N) pl[(size_t)(s.scan ? 0 : tid) * WL + (size_t)s_px[tid] * L + s_py[tid]] = 1;
+  if (tid == 0) s.full[e] = 0;
+}
+
+// LDS bytes of sg_erode_kernel: two bitboards, per-cell d (u8), the value LUT
+__host__ __device__ inline size_t erode_lds_bytes(int W, int L) {
+  const size_t nw = (size_t)W * ((L + 63) / 64);
+  return 2 * nw * 8 + (((size_t)W * L + 15) & ~(size_t)15) + (((size_t)(W + L + 1) * 4 + 15) & ~(size_t)15);
+}
+
+// Distance layer by bit-parallel erosion (maps with W + L <= 257 whose
+// planes fit LDS; every BASELINE-sized map).  With C = the sensed cells and
+// cells outside the grid counting as non-sources (OpenCV's border), the L1
+// distance to the nearest source is d(c) = #{k >= 0 : c in E_k}, E_0 = C,
+// E_{k+1} = E_k & (its four 1-cell shifts): an L1 ball of radius k+1 is the
+// radius-k ball grown by one 4-neighbour step.  A cell leaving at step k has
+// d = k + 1; max(d) = the number of non-empty layers.  Each step is a few
+// word ops per 64 cells, and max(d) is small (obstacles are sources), so the
+// kernel is bound by the float32 layer write: per 4 cells one u32 of d from
+// LDS, four LUT reads (1 - d/M, the reference's float32 steps), one 16-B store.
+__global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_px[kMaxAgents], s_py[kMaxAgents];
+  const int e = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
+  const int W = s.W, L = s.L, RW = s.RW;
+  const int nw = W * RW;
+  const size_t WL = (size_t)W * L;
+  if (s.full[e]) write_full_layers(s, e, tid, NT, s_px, s_py);
+  uint64_t* cur = reinterpret_cast<uint64_t*>(smem);
+  uint64_t* nxt = cur + nw;
+  uint8_t* d8 = reinterpret_cast<uint8_t*>(nxt + nw);
+  float* lut = reinterpret_cast<float*>(d8 + ((WL + 15) & ~(size_t)15));
+  const uint64_t* cov = s.cov + (size_t)e * nw;
+  const uint64_t inval_last = (L & 63) ? ~low_mask(L & 63) : 0ull;  // bits >= L of a row's last word
+  for (size_t i = tid; i < (WL + 15) / 16; i += NT) reinterpret_cast<uint4*>(d8)[i] = make_uint4(0, 0, 0, 0);
+  int any_src = 0, any_cov = 0;
+  for (int i = tid; i < nw; i += NT) {
+    const int w = i % RW;
+    const uint64_t inval = (w == RW - 1) ? inval_last : 0ull;
+    const uint64_t c = cov[i] & ~inval;
+    cur[i] = c | inval;
+    any_src |= (~c & ~inval) != 0ull;
+    any_cov |= c != 0ull;
+  }
+  any_src = __syncthreads_or(any_src);
+  any_cov = __syncthreads_or(any_cov);
+  float* out = s.dist_plane + (size_t)e * WL;
+  if (!any_src) {  // no source cell: SciPy's -1 everywhere -> 1 - (-1)
+    for (size_t i = tid; i < WL; i += NT) out[i] = 2.0f;
+    return;
+  }
+  int M = 0;
+  if (any_cov) {
+    for (int k = 0;; ++k) {
+      int nz = 0;
+      for (int i = tid; i < nw; i += NT) {
+        const int u = i / RW, w = i - u * RW;
+        const uint64_t inval = (w == RW - 1) ? inval_last : 0ull;
+        const uint64_t c = cur[i];
+        const uint64_t up = u > 0 ? cur[i - RW] : ~0ull;
+        const uint64_t dn = u < W - 1 ? cur[i + RW] : ~0ull;
+        const uint64_t lw = w > 0 ? cur[i - 1] : ~0ull;
+        const uint64_t rw = w < RW - 1 ? cur[i + 1] : ~0ull;
+        const uint64_t n = (c & up & dn & ((c << 1) | (lw >> 63)) & ((c >> 1) | (rw << 63))) | inval;
+        nxt[i] = n;
+        uint64_t leave = c & ~n;
+        if (leave) {
+          uint8_t* row = d8 + (size_t)u * L + (w << 6);
+          const uint8_t dk = (uint8_t)(k + 1);
+          for (; leave; leave &= leave - 1) row[__ffsll((unsigned long long)leave) - 1] = dk;
+        }
+        nz |= (n & ~inval) != 0ull;
+      }
+      if (!__syncthreads_or(nz)) {
+        M = k + 1;
+        break;
+      }
+      uint64_t* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+  }
+  const float Mf = (float)M;
+  for (int d = tid; d <= M; d += NT) lut[d] = dist_value((float)d, Mf);
+  __syncthreads();
+  if ((L & 3) == 0) {
+    const uint32_t* d4 = reinterpret_cast<const uint32_t*>(d8);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    for (size_t g = tid; g < WL / 4; g += NT) {
+      const uint32_t q = d4[g];
+      o4[g] = make_float4(lut[q & 255u], lut[(q >> 8) & 255u], lut[(q >> 16) & 255u], lut[q >> 24]);
+    }
+  } else {
+    for (size_t i = tid; i < WL; i += NT) out[i] = lut[d8[i]];
+  }
+}
+
+// Distance layer by separable sweeps (any map up to kMaxSide): a row pass
+// (distance along the row) and down/up min-plus column sweeps over u16
+// planes in LDS or, when they do not fit, the global scratch.
 template <bool kLds>
 __global__ __launch_bounds__(256) void sg_dist_kernel(SState s, int pitch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_px[kMaxAgents], s_py[kMaxAgents];
   __shared__ int s_max;
   const int e = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
-  const int W = s.W, L = s.L, RW = s.RW, N = s.N;
+  const int W = s.W, L = s.L, RW = s.RW;
   const size_t mw = (size_t)W * RW, WL = (size_t)W * L;
   const uint64_t* cov = s.cov + (size_t)e * mw;
   uint16_t* H = kLds ? reinterpret_cast<uint16_t*>(smem) : s.scratch + (size_t)e * W * pitch;
   if (tid == 0) s_max = 0;
-
-  if (s.full[e]) {  // uniform: rewrite every uint8 layer
-    if (tid < N) {
-      s_px[tid] = s.pos[((size_t)e * N + tid) * 2];
-      s_py[tid] = s.pos[((size_t)e * N + tid) * 2 + 1];
-    }
-    uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
-    const uint64_t* ob = s.obst + (size_t)e * mw;
-    for (size_t i = tid; i < WL; i += NT) {
-      const int u = div_L(s, (int)i), v = (int)i - u * L;
-      const size_t wi = (size_t)u * RW + (v >> 6);
-      const int b = v & 63;
-      for (int p = 0; p < s.P; ++p) pl[(size_t)p * WL + i] = 0;
-      pl[(size_t)s.P * WL + i] = (uint8_t)((ob[wi] >> b) & 1ull);
-      pl[(size_t)(s.P + 1) * WL + i] = (uint8_t)(((cov[wi] >> b) & 1ull) ^ 1ull);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid < N) pl[(size_t)(s.scan ? 0 : tid) * WL + (size_t)s_px[tid] * L + s_py[tid]] = 1;
-    if (tid == 0) s.full[e] = 0;
-  }
+  if (s.full[e]) write_full_layers(s, e, tid, NT, s_px, s_py);
 
   // row pass: H[u][v] = distance along row u to the nearest source (_free != 0)
   for (int u = tid; u < W; u += NT) {
@@ -578,6 +681,8 @@ struct SgEnv {
   int device = 0;
   int pitch = 0;      // u16 elements per distance-plane row
   bool lds = true;    // distance planes in LDS (else s.scratch)
+  bool erode = false; // sg_erode_kernel (else the sweep kernel)
+  size_t erode_lds = 0;
   int dist_nt = 256;
   bool grids_set = false;
   bool stale = true;  // the dist layer does not describe the current maps
@@ -628,6 +733,10 @@ int sg_ready(SgEnv* E, const char* who) {
 }
 
 hipError_t launch_dist(SgEnv* E, hipStream_t st) {
+  if (E->erode) {
+    hipLaunchKernelGGL(mcs::sg_erode_kernel, dim3(E->s.B), dim3(256), E->erode_lds, st, E->s);
+    return hipGetLastError();
+  }
   const size_t lds = E->lds ? (size_t)E->s.W * E->pitch * 2 : 0;
   if (E->lds)
     hipLaunchKernelGGL(mcs::sg_dist_kernel<true>, dim3(E->s.B), dim3(E->dist_nt), lds, st, E->s, E->pitch);
@@ -695,6 +804,12 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   E->pitch = ((c.length + 1) / 2) * 2;
   if (((E->pitch / 2) & 1) == 0) E->pitch += 2;
   E->lds = (size_t)c.width * E->pitch * 2 <= mcs::kLdsLimit;
+  E->erode_lds = mcs::erode_lds_bytes(c.width, c.length);
+  static const bool force_sweep = [] {  // MARLCOV_SG_SWEEP=1: A/B against the sweep kernel
+    const char* v = getenv("MARLCOV_SG_SWEEP");
+    return v && atoi(v) == 1;
+  }();
+  E->erode = !force_sweep && c.width + c.length <= 257 && E->erode_lds <= mcs::kLdsLimit;
   const int side = c.width > c.length ? c.width : c.length;
   E->dist_nt = side <= 64 ? 64 : (side <= 128 ? 128 : 256);
   const size_t B = s.B, N = s.N, G = s.G, mw = (size_t)s.W * s.RW;

@@ -109,7 +109,11 @@ BATCH_CASES = {
     "n16_r2_dist": (sg_cfg(numrobot=16, senseradius=2, free_penalty=0.1, dist_reward=1), (64, 64), 0.1, 8, 30),
     "scan_n40_pairwise_sum": (sg_cfg(numrobot=40, use_scanning=1, free_penalty=0.15, dist_reward=1,
                                      collision_penalty=0.75), (24, 24), 0.1, 6, 30),
+    # W + L > 257: the separable sweep kernel instead of the erosion kernel,
+    # with its u16 planes in the global scratch / in LDS
     "global_scratch_150x300": (sg_cfg(numrobot=4, senseradius=2, dist_reward=1), (150, 300), 0.1, 4, 25),
+    "sweep_lds_200x100": (sg_cfg(numrobot=3, senseradius=2, dist_reward=1), (200, 100), 0.02, 4, 25),
+    "erode_open_grid_1x250": (sg_cfg(numrobot=2, senseradius=3, dist_reward=1), (1, 250), 0.0, 4, 60),
     "done_incr_small": (sg_cfg(numrobot=3, senseradius=2, done_thresh=0.3, done_incr=0.25, dist_reward=1),
                         (14, 14), 0.1, 10, 80),
     "r15_wide_window": (sg_cfg(numrobot=2, senseradius=15, free_penalty=0.05, dist_reward=1), (70, 90), 0.1, 4, 20),
