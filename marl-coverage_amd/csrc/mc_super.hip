@@ -237,8 +237,17 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
   if (e >= s.B) return;
   const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = s.r;
   const bool me = lane < N;
+  // every load that depends only on e is issued up front (one round trip)
+  const int my_act = me ? (int)actions[(size_t)e * N + lane] : 255;  // slot `lane`'s action byte
+  const int g = s.env_grid[e];
+  const int q = quot ? quot[e] : 0;
+  const int ap = s.a_prev[e];
+  const int cs0 = s.currstep[e];
+  const uint32_t cc0 = s.cov_cnt[e];
+  const double dt = s.done_thresh[e];
+  const int npos = s.numpos[g];
   bool is_done;
-  if (actions[(size_t)e * N] == 255) {  // action == -1 / None (:88-90)
+  if (__shfl(my_act, 0) == 255) {  // action == -1 / None (:88-90)
     is_done = true;
     if (lane == 0) {
       reward[e] = 0.0;
@@ -246,7 +255,6 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     }
   } else {
     const size_t mw = (size_t)W * RW;
-    const int g = s.env_grid[e];
     const uint64_t* gneg = s.gneg + (size_t)g * mw;
     const uint64_t* gpos = s.gpos + (size_t)g * mw;
     uint64_t* cov = s.cov + (size_t)e * mw;
@@ -265,7 +273,8 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
       for (int j = 0; j < N; ++j) rank += __shfl(sc, j) < sc;
       slot = rank;
     }
-    const int u = me ? (int)actions[(size_t)e * N + slot] : 255;
+    const int slot_act = __shfl(my_act, slot);
+    const int u = me ? slot_act : 255;
     int tx = x, ty = y;
     if (u == 0) tx = x - 1;
     else if (u == 1) tx = x + 1;
@@ -359,8 +368,6 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
 
     // motion_penalty(a) on every slot (:203-208, 227-243): a is the quotient
     // left in `action` after the digit loop; a == inv(a) never holds
-    const int q = quot ? quot[e] : 0;
-    const int ap = s.a_prev[e];
     if ((q < 0 || q >= 4) && lane == 0) atomicOr(s.err, ERR_KEY);
     v = v + ((q == ap) ? 0.0 : -1.0);
     if (me) {
@@ -373,10 +380,9 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     int dn = 0;
     if (lane == 0) {
       double total = np_pairwise_sum(s_v[w], N);
-      const int cs = s.currstep[e] + 1;
-      const uint32_t cc = s.cov_cnt[e] + (uint32_t)cnt;
-      const double pc = (double)cc / (double)s.numpos[g];
-      const double dt = s.done_thresh[e];
+      const int cs = cs0 + 1;
+      const uint32_t cc = cc0 + (uint32_t)cnt;
+      const double pc = (double)cc / (double)npos;
       const bool cond = (dt < 1.0 ? dt : 1.0) <= pc;  // min(_done_thresh, 1) <= percent_covered()
       if (cond) total = total + s.term;
       if (cond) s.done_thresh[e] = dt + s.dincr;  // done() (:408-411)
