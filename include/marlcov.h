@@ -127,7 +127,11 @@ enum {
                                 with d == M, (x << 16) | (y & 0xFFFF), map coords */
   MC_FIELD_DIST_LISTED = 15, /* uint32 [1] maps the last POST sent to the full
                                 transform (read-only diagnostic)               */
-  MC_FIELD_COUNT = 16
+  /* episode record (read-only), written when an env reports done, before an
+     auto-reset clears the counters: the Utils/utils.py:141 statistic       */
+  MC_FIELD_EP_PC = 16,       /* double [B] percent_covered() at the episode end */
+  MC_FIELD_EP_LEN = 17,      /* int32  [B] _currstep at the episode end        */
+  MC_FIELD_COUNT = 18
 };
 
 int32_t mc_abi_version(void);
@@ -172,8 +176,9 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos,
 /* One step of every env (dec_grid_rl.py:91-169) with per-agent action bytes
  * dev_actions uint8 [B][N] (MC_ACT_*).  Writes reward float64 [B], done uint8
  * [B], obs uint8 [B][N][Lc][E][E] and optionally the comm graph [B][N][N].
- * With cfg.auto_reset, an env that reports done is reset in the same launch
- * and its obs are the first obs of the new episode. */
+ * With cfg.auto_reset, an env that reports done (the sentinel step included)
+ * is reset in the same launch and its obs are the first obs of the new
+ * episode; MC_FIELD_EP_PC / EP_LEN keep the finished episode's record. */
 int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward,
             uint8_t* dev_done, void* dev_obs, uint8_t* dev_adj, void* stream);
 

@@ -20,6 +20,9 @@ def __getattr__(name):
     if name in ("DecGridRL", "decode_action"):
         from . import dec_grid_rl
         return getattr(dec_grid_rl, name)
+    if name == "episodes":
+        from . import episodes
+        return episodes
     if name in ("SuperGridRL", "BatchSuperGridEnv", "decode_super_action"):
         from . import super_env
         return getattr(super_env, name)

@@ -103,6 +103,8 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_GRID_POS: return {(void*)s.grid_pos, G * mw * 8};
     case MC_FIELD_DIST_MW: return {s.dist_mw, s.dist_mw ? B * N * 8 : -1};
     case MC_FIELD_DIST_LISTED: return {E->dist_list, E->dist_list ? 4 : -1};
+    case MC_FIELD_EP_PC: return {s.ep_pc, B * 8};
+    case MC_FIELD_EP_LEN: return {s.ep_len, B * 4};
     default: return {nullptr, -1};
   }
 }
@@ -286,6 +288,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   ALLOC(s.done_thresh, double, B);
   ALLOC(s.episode, uint32_t, B);
   ALLOC(s.err, uint32_t, 4);
+  ALLOC(s.ep_pc, double, B);
+  ALLOC(s.ep_len, int32_t, B);
 #undef ALLOC
   s.grid_neg = gneg;
   s.grid_pos = gpos;
@@ -616,7 +620,7 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   if (!E || !dev_src) return fail(MC_EINVAL, "mc_set_state: null argument");
   FieldDesc d = field(E, f);
   if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
-  if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED)
+  if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED || f == MC_FIELD_EP_PC || f == MC_FIELD_EP_LEN)
     return fail(MC_EINVAL, "field %d is derived state (read-only)", f);
   if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   HIP_TRY(hipSetDevice(E->device));

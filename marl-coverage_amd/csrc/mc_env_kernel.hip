@@ -968,6 +968,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   const bool sentinel = valid && is_step && act0 == 255;
   const bool reset_req = valid && !is_step && req != 0;
   const bool active = valid && is_step && !sentinel;
+  const bool sent_reset = sentinel && s.auto_reset;  // a sentinel's done resets too
   if (C.sub < N) {
     set_agent<WT>(s, L, C.sub, p0.x, p0.y);
     L.act[C.sub] = (uint8_t)act;
@@ -1040,6 +1041,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       else if (cs == s.maxsteps) done = true;                // :544-545
       reward_out[e] = r;
       done_out[e] = done ? 1 : 0;
+      if (done) {  // the episode record (Utils/utils.py:138-141)
+        s.ep_pc[e] = pc;
+        s.ep_len[e] = cs;
+      }
       s.free_cnt[e] = fc;
       s.vis_cnt[e] = vc;
       s.currstep[e] = cs;
@@ -1054,29 +1059,37 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     } else {
       reset_env<NT, EPW, WT, SUK>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
-  } else if (reset_req) {
-    reset_env<NT, EPW, WT, SUK>(s, C, inj_pos);
+  } else if (reset_req || sent_reset) {
+    if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
+      reward_out[e] = 0.0;
+      done_out[e] = 1;
+      s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
+      s.ep_len[e] = currstep0;
+    }
+    reset_env<NT, EPW, WT, SUK>(s, C, reset_req ? inj_pos : nullptr);
   } else {
-    // sentinel step / env left out of a partial reset: obs of the current
-    // state only (dec_grid_rl.py:104-107,160)
+    // sentinel step without auto-reset / env left out of a partial reset:
+    // obs of the current state only (dec_grid_rl.py:104-107,160)
     Items<KI> I;
     stage<NT, EPW, WT, KI>(s, C, g0, true, I);
     stage_fold<NT, EPW, WT, KI>(s, C, I);
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
+      s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
+      s.ep_len[e] = currstep0;
     }
   }
   __syncthreads();
 
-  if (active || reset_req) {
+  if (active || reset_req || sent_reset) {
     if (C.sub < N)
       reinterpret_cast<int2*>(s.pos)[(size_t)e * N + C.sub] = make_int2(L.x[C.sub], L.y[C.sub]);
     if (C.sub == 0) s.moved[e] = L.sc->moved;
     // dist_reward: a reset map, or one whose witness got closer than M,
     // has an unknown M now (recomputed by the full transform, mc_dist.hip)
     if (s.dist && C.sub < N &&
-        (reset_req || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
+        (reset_req || sent_reset || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
   }
   STAMP(8);

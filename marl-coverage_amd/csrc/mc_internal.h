@@ -92,6 +92,10 @@ struct State {
   // sets M = -1 when sensing covers a cell closer than M to the witness (or
   // the env resets); otherwise M is unchanged (mc_dist.hip).
   int32_t* dist_mw;
+  // episode record, written when an env reports done (before an auto-reset
+  // clears the counters): percent_covered() and _currstep at the end
+  double* ep_pc;
+  int32_t* ep_len;
 };
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane

@@ -217,15 +217,21 @@ def test_auto_reset_matches_oracle_reset(torch_cuda, dist):
     st = device_state(env)
     refs = [oracle_from_device(st, b, cfg) for b in range(B)]
     resets = 0
+    from marlcov import _lib
     for t in range(20):
         acts = rs.randint(0, 4, size=(B, 3)).astype(np.uint8)
+        acts[rs.rand(B) < 0.08, 0] = 255  # a sentinel's done resets the env too
         obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
         obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
         st = device_state(env)
+        ep_pc = env.get_state(_lib.FIELD_EP_PC).cpu().numpy()
+        ep_len = env.get_state(_lib.FIELD_EP_LEN).cpu().numpy()
         for b in range(B):
             o, r, d = refs[b].step(ref_action(acts[b]))
             assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), (t, b)
             if d:
+                # the episode record: utils.py:141's percent_covered() and the length
+                assert ep_pc[b] == refs[b].percent_covered() and ep_len[b] == refs[b]._currstep, (t, b)
                 resets += 1
                 p = st["pos"][b]
                 assert len({tuple(q) for q in p}) == 3
