@@ -88,6 +88,8 @@ typedef struct mc_config {
   int32_t auto_reset;         /* batch extra: re-place agents on done         */
   int32_t reset_grid_mode;    /* 0: keep the env's grid on reset;
                                  1: draw a grid uniformly from the pool       */
+  int32_t mini_map_rad;       /* 'mini_map_rad' (> 0: float64 minimap layers
+                                 3-4 via mc_set_minimap_obs; pad >= it)       */
   uint64_t seed;              /* batch extra: device Philox seed              */
 } mc_config;
 
@@ -97,7 +99,8 @@ typedef struct mc_layout {
   int32_t tile_cols;          /* ceil(length / 8) rounded up to a multiple of 4 */
   int32_t window_half;        /* H = max(ceil(range), egoradius)              */
   int32_t window_tiles;       /* TW: tiles per side staged per agent          */
-  int32_t obs_layers;         /* Lc (3 + dist_reward + dijkstra_input)        */
+  int32_t obs_layers;         /* Lc ((mini_map_rad > 0 ? 5 : 3) + dist_reward
+                                 + dijkstra_input, dec_grid_rl.py:322-332)    */
   int32_t obs_side;           /* E = 2*egoradius + 1                          */
   int64_t obs_bytes_per_env;  /* N*Lc*E*E (uint8 obs)                         */
   int64_t mask_words_per_agent; /* tile_rows * tile_cols (one map)            */
@@ -195,6 +198,14 @@ int mc_set_state(void* env, int32_t field, const void* dev_src, int64_t bytes, v
  * dijkstra_input as well, layer 3 of the uint8 obs is the dijkstra path and
  * layer 4 is 0, as in the reference (the dist crop is overwritten, :354). */
 int mc_set_dist_obs(void* env, float* dev_dist_obs);
+
+/* mini_map_rad > 0 (dec_grid_rl.py:360-370): register the caller's float64
+ * [B][N][2][E][E] buffer that every mc_reset / mc_step fills with obs layers 3
+ * and 4, cv2.resize(INTER_LINEAR) of the agent's free / obstacle maps cropped
+ * with radius mini_map_rad (OpenCV's generic CV_64F path; parity vs OpenCV
+ * unpinned).  The uint8 obs hold 0 in layers 3.. (the minimap overwrites the
+ * dist / dijkstra layer in the reference).  Required before the first reset. */
+int mc_set_minimap_obs(void* env, double* dev_minimap_obs);
 
 /* Synchronise `stream` and report (then clear) the device error word. */
 int mc_check(void* env, void* stream);

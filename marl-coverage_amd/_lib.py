@@ -51,6 +51,7 @@ class McConfig(ctypes.Structure):
         ("dijkstra_input", ctypes.c_int32),
         ("auto_reset", ctypes.c_int32),
         ("reset_grid_mode", ctypes.c_int32),
+        ("mini_map_rad", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
     ]
 
@@ -134,6 +135,7 @@ SIGNATURES = [
     ("mc_check", ctypes.c_int, [_VP, _VP]),
     ("mc_debug_stamps", ctypes.c_int, [_VP, _VP]),
     ("mc_set_dist_obs", ctypes.c_int, [_VP, _VP]),
+    ("mc_set_minimap_obs", ctypes.c_int, [_VP, _VP]),
     ("mc_sg_create", ctypes.c_int, [ctypes.POINTER(McSgConfig), ctypes.c_int, ctypes.POINTER(_VP)]),
     ("mc_sg_destroy", None, [_VP]),
     ("mc_sg_query", ctypes.c_int, [_VP, ctypes.POINTER(McSgLayout)]),

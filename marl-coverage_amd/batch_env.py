@@ -82,8 +82,6 @@ class BatchCoverageEnv:
         self.sensor = sensor if sensor is not None else make_sensor(self.config)
         ego = int(self.config["egoradius"])
         mini = int(self.config.get("mini_map_rad", 0))
-        if mini > 0:
-            raise NotImplementedError("mini_map_rad > 0 (cv2.resize minimap layers) is not built")
         self.pad = max(ego, mini)
 
         if (grids is None) == (gen is None):
@@ -113,6 +111,7 @@ class BatchCoverageEnv:
             c.square_radius = self.sensor._radius
         c.egoradius = ego
         c.pad = self.pad
+        c.mini_map_rad = mini
         c.collision_penalty = float(self.config["collision_penalty"])
         c.terminal_reward = float(self.config["terminal_reward"])
         c.done_thresh = float(self.config["done_thresh"])
@@ -168,6 +167,12 @@ class BatchCoverageEnv:
             E = lay.obs_side
             self.dist_obs = torch.zeros((B, N, E, E), dtype=torch.float32, device=dev)
             _lib.check(self.lib.mc_set_dist_obs(self._h, self.dist_obs.data_ptr()), "mc_set_dist_obs")
+        # mini_map_rad: the float64 minimap layers (obs layers 3 and 4)
+        self.minimap_obs = None
+        if mini > 0:
+            E = lay.obs_side
+            self.minimap_obs = torch.zeros((B, N, 2, E, E), dtype=torch.float64, device=dev)
+            _lib.check(self.lib.mc_set_minimap_obs(self._h, self.minimap_obs.data_ptr()), "mc_set_minimap_obs")
 
     # ------------------------------------------------------------------
     def _stream(self):

@@ -32,6 +32,7 @@ hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist
 size_t dist_lds_bytes(const State& s, int pad);
 int dist_max_rows();
 size_t dijkstra_lds_bytes(const State& s, int pad);
+hipError_t launch_minimap(const State& s, int mini, double* out, hipStream_t stream);
 __global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
 }  // namespace mc
 
@@ -68,6 +69,7 @@ struct Env {
   size_t dt_lds = 0;  // dist_reward: LDS bytes of the distance kernel
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
+  double* mini_obs = nullptr; // mini_map_rad: caller's float64 [B][N][2][E][E]
   uint32_t* dist_list = nullptr;  // dist_reward: [B*N] maps for the full transform + count
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
@@ -183,6 +185,9 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     return fail(MC_EINVAL, "square sensor range must be >= 0");
   if (c.egoradius < 0) return fail(MC_EINVAL, "egoradius must be >= 0");
   if (c.pad < c.egoradius) return fail(MC_EINVAL, "pad must be >= egoradius");
+  if (c.mini_map_rad < 0 || c.pad < c.mini_map_rad) return fail(MC_EINVAL, "need 0 <= mini_map_rad <= pad");
+  if (c.mini_map_rad > 0 && 2 * c.egoradius + 1 > 32)
+    return fail(MC_EINVAL, "minimap layers need egoradius <= 15");
   if (!(c.lidar_range == c.lidar_range)) return fail(MC_EINVAL, "lidar range is NaN");
   if (c.maxsteps < 0) return fail(MC_EINVAL, "maxsteps must be >= 0");
 
@@ -238,7 +243,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.mg_TW2 = mc::magic_div((uint32_t)(TW * TW));
   s.ego = c.egoradius;
   s.E = 2 * c.egoradius + 1;
-  s.Lc = 3 + (c.dist_reward ? 1 : 0) + (c.dijkstra_input ? 1 : 0);
+  s.Lc = (c.mini_map_rad > 0 ? 5 : 3) + (c.dist_reward ? 1 : 0) + (c.dijkstra_input ? 1 : 0);
   s.dist = c.dist_reward ? 1 : 0;
   s.mg_LcE = mc::magic_div((uint32_t)(s.Lc * s.E));
   s.mg_E = mc::magic_div((uint32_t)s.E);
@@ -532,6 +537,10 @@ int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {
 // dijkstra_input: obs layer 3 from the post-step maps (dec_grid_rl.py:354-358),
 // a second kernel on the same stream
 static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
+  if (E->cfg.mini_map_rad > 0) {  // the minimap overwrites layer 3 (dec_grid_rl.py:365)
+    HIP_TRY(mc::launch_minimap(E->s, E->cfg.mini_map_rad, E->mini_obs, st));
+    return MC_OK;
+  }
   if (!E->cfg.dijkstra_input) return MC_OK;
   if (E->dj_lds > 65536)
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dijkstra_kernel),
@@ -558,6 +567,8 @@ static int ready(Env* E, const char* who) {
   if (!E->grids_set) return fail(MC_ESTATE, "%s: grids not set (mc_set_grids / mc_generate_grids)", who);
   if (E->cfg.dist_reward && !E->dist_obs)
     return fail(MC_ESTATE, "%s: dist_reward needs the float obs buffer (mc_set_dist_obs)", who);
+  if (E->cfg.mini_map_rad > 0 && !E->mini_obs)
+    return fail(MC_ESTATE, "%s: mini_map_rad needs the float64 minimap buffer (mc_set_minimap_obs)", who);
   return MC_OK;
 }
 
@@ -637,6 +648,14 @@ int mc_set_dist_obs(void* env, float* dev_dist_obs) {
   if (!E || !dev_dist_obs) return fail(MC_EINVAL, "mc_set_dist_obs: null argument");
   if (!E->cfg.dist_reward) return fail(MC_EINVAL, "mc_set_dist_obs: config has dist_reward = 0");
   E->dist_obs = dev_dist_obs;
+  return MC_OK;
+}
+
+int mc_set_minimap_obs(void* env, double* dev_minimap_obs) {
+  Env* E = as_env(env);
+  if (!E || !dev_minimap_obs) return fail(MC_EINVAL, "mc_set_minimap_obs: null argument");
+  if (E->cfg.mini_map_rad <= 0) return fail(MC_EINVAL, "mc_set_minimap_obs: config has mini_map_rad = 0");
+  E->mini_obs = dev_minimap_obs;
   return MC_OK;
 }
 

@@ -203,6 +203,8 @@ class DecGridRL:
         if env.dist_obs is not None and not self._dijkstra_input:
             # float distance layer (the dijkstra path overwrites it, :354-358)
             self._obs_np[:, 3] = env.dist_obs[0].cpu().numpy().astype(np.float64)
+        if env.minimap_obs is not None:  # overwrites layers 3 and 4 (:365-370)
+            self._obs_np[:, 3:5] = env.minimap_obs[0].cpu().numpy()
         pos = env.get_state(_lib.FIELD_POS)[0].cpu().numpy()
         self._xinds = pos[:, 0].astype(int)
         self._yinds = pos[:, 1].astype(int)

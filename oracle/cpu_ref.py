@@ -24,8 +24,10 @@ library itself:
     (``dec_grid_rl.py:273-275``); cv2 is not installed, so both the oracle and
     the golden capture use the exact-L1 SciPy restatement below.  Parity with
     real OpenCV: *unpinned*.
-  * ``mini_map_rad > 0`` needs ``cv2.resize(INTER_LINEAR)``
-    (``dec_grid_rl.py:360-370``): not restated, raises NotImplementedError.
+  * ``mini_map_rad > 0`` uses ``cv2.resize(INTER_LINEAR)``
+    (``dec_grid_rl.py:360-370``); ``cv2_resize_linear`` restates OpenCV's
+    generic CV_64F path (the golden capture uses the same restatement).
+    Parity with real OpenCV: *unpinned*.
 """
 from __future__ import annotations
 
@@ -141,6 +143,69 @@ def l1_distance_to_covered(free: np.ndarray) -> np.ndarray:
     return distance_transform_cdt(inv, metric="taxicab").astype(np.float32)
 
 
+def _linear_taps(src_n: int, dst_n: int):
+    """OpenCV's INTER_LINEAR tap tables (resizeGeneric_ set-up in
+    imgproc/src/resize.cpp, non-area mode): per destination index the source
+    index, the float32 weights (1 - f, f), and ``xmax`` (from there on the
+    horizontal pass copies ``S[xofs]``).  ``inv_scale = dst/src`` and
+    ``scale = 1/inv_scale`` in double, ``f = (float)((d + 0.5)*scale - 0.5)``,
+    ``s = floor(f)``, ``f -= s`` in float; the horizontal indices are clamped
+    (s < 0 -> 0, f = 0; s >= n - 1 -> n - 1, f = 0), the vertical ones are
+    clipped when rows are fetched."""
+    inv_scale = dst_n / src_n
+    scale = 1.0 / inv_scale
+    xofs, yofs, alpha, beta = [], [], [], []
+    xmax = dst_n
+    for d in range(dst_n):
+        f = np.float32((d + 0.5) * scale - 0.5)
+        s = int(np.floor(f))
+        f = np.float32(f - np.float32(s))
+        yofs.append(s)
+        beta.append((np.float32(np.float32(1.0) - f), f))
+        fx, sx = f, s
+        if sx < 0:
+            fx, sx = np.float32(0.0), 0
+        if sx + 1 >= src_n:
+            xmax = min(xmax, d)
+            if sx >= src_n - 1:
+                fx, sx = np.float32(0.0), src_n - 1
+        xofs.append(sx)
+        alpha.append((np.float32(np.float32(1.0) - fx), fx))
+    return xofs, alpha, xmax, yofs, beta
+
+
+def cv2_resize_linear(src: np.ndarray, dst_n: int) -> np.ndarray:
+    """Restated ``cv2.resize(src, (dst_n, dst_n), interpolation=INTER_LINEAR)``
+    for a square float64 image (``dec_grid_rl.py:365-370``): OpenCV's generic
+    path for CV_64F, ``HResizeLinear<double, double, float>`` then
+    ``VResizeLinear<double, double, float>`` — double arithmetic with float
+    weights, horizontal pass first, no FMA.  cv2 is absent: parity with real
+    OpenCV (its version, IPP/HAL dispatch) is *unpinned*."""
+    n = src.shape[0]
+    if src.shape != (n, n):
+        raise ValueError("square source expected")
+    if dst_n == n:  # cv::resize copies when the sizes match
+        return src.astype(np.float64).copy()
+    xofs, alpha, xmax, yofs, beta = _linear_taps(n, dst_n)
+    h = np.empty((n, dst_n))
+    for r in range(n):
+        row = src[r]
+        for d in range(dst_n):
+            sx = xofs[d]
+            if d < xmax:
+                h[r, d] = float(row[sx]) * float(alpha[d][0]) + float(row[sx + 1]) * float(alpha[d][1])
+            else:
+                h[r, d] = float(row[sx])
+    out = np.empty((dst_n, dst_n))
+    for d in range(dst_n):
+        r0 = min(max(yofs[d], 0), n - 1)
+        r1 = min(max(yofs[d] + 1, 0), n - 1)
+        b0, b1 = float(beta[d][0]), float(beta[d][1])
+        for c in range(dst_n):
+            out[d, c] = h[r0, c] * b0 + h[r1, c] * b1
+    return out
+
+
 def distance_map(free: np.ndarray) -> np.ndarray:
     """``DecGridRL.get_distance_map`` (``dec_grid_rl.py:260-282``)."""
     d = l1_distance_to_covered(free)
@@ -241,8 +306,6 @@ class DecGridRLRef:
         self._single_square_tool = c["single_square_tool"]
         self._dijkstra_input = c["dijkstra_input"]
         self._sensor = make_sensor(c)
-        if self._mini_map_rad > 0:
-            raise NotImplementedError("mini_map_rad > 0 needs cv2.resize (unpinned)")
         self._pad = max(self._egoradius, self._mini_map_rad)          # :78
         self.reset(False, None)                                          # :81
         self._obs_dim = self.get_egocentric_observations()[0].shape    # :84
@@ -356,6 +419,10 @@ class DecGridRLRef:
                 path = dijkstra_path_map(self._free_pad[i] - self._obst_pad[i],
                                          x + p, y + p)
                 z[i][3] = self.arraySubset(path, x, y, e)
+            if self._mini_map_rad > 0:  # :360-370, overwrites layers 3 and 4
+                m = self._mini_map_rad
+                z[i][3] = cv2_resize_linear(self.arraySubset(self._free_pad[i], x, y, m), 2 * e + 1)
+                z[i][4] = cv2_resize_linear(self.arraySubset(self._obst_pad[i], x, y, m), 2 * e + 1)
         return z
 
     def updateCommmunicationGraph(self):

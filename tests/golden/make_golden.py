@@ -14,6 +14,7 @@ Nothing else of the reference is modified.  The fixtures written here
 travels to the GPU box.
 
     python tests/golden/make_golden.py            # rewrite all fixtures
+    python tests/golden/make_golden.py minimap_   # only the cases with this prefix
 """
 from __future__ import annotations
 
@@ -45,6 +46,19 @@ def _install_stubs():
         return distance_transform_cdt(src, metric="taxicab").astype(np.float32)
 
     cv2.distanceTransform = distanceTransform
+
+    # cv2.resize(INTER_LINEAR) of the minimap layers (dec_grid_rl.py:365-370):
+    # the oracle's restatement of OpenCV's generic CV_64F path, so these cases
+    # pin the reference's crop / layer logic around it (resize itself unpinned)
+    cv2.INTER_LINEAR = 1
+
+    def resize(src, dsize, interpolation):
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        from oracle.cpu_ref import cv2_resize_linear
+        assert interpolation == cv2.INTER_LINEAR and dsize[0] == dsize[1]
+        return cv2_resize_linear(np.asarray(src, dtype=np.float64), dsize[0])
+
+    cv2.resize = resize
     sys.modules["cv2"] = cv2
 
 
@@ -221,6 +235,24 @@ def build_cases(gridload):
     add("crowded_collisions_n8", cfg(numrobot=8, collision_penalty=2,
                                      sensor_config={"num_lasers": 9, "range": 4}),
         [g], seed=21, events=[("reset", False, None)] + joint_ints(rs, 8, 60))
+
+    # minimap layers (mini_map_rad > 0, dec_grid_rl.py:360-370): the template
+    # config's shape (egoradius 5, mini_map_rad 10, comm + map sharing), a
+    # down-scale with the dist and dijkstra layers underneath, an up-scale
+    g = bernoulli(rs, 30, 30, 0.15)
+    add("minimap_template_ego5_mini10",
+        cfg(numrobot=2, egoradius=5, mini_map_rad=10, comm_radius=10, allow_comm=1, map_sharing=1,
+            sensor_config={"num_lasers": 21, "range": 6}),
+        [g], use_graph=True, seed=22, events=[("reset", False, None)] + joint_ints(rs, 2, 40))
+    g = bernoulli(rs, 24, 24, 0.1)
+    add("minimap_dist_dijkstra_square",
+        cfg(numrobot=2, mini_map_rad=4, dist_reward=1, dijkstra_input=1, sensor_type="square_sensor",
+            sensor_config={"range": 2}),
+        [g], seed=23, events=[("reset", False, None)] + joint_ints(rs, 2, 30))
+    g = bernoulli(rs, 20, 20, 0.1)
+    add("minimap_upscale_ego3_mini1",
+        cfg(numrobot=1, egoradius=3, mini_map_rad=1, sensor_config={"num_lasers": 7, "range": 3}),
+        [g], seed=24, events=[("reset", False, None)] + joint_ints(rs, 1, 30))
     return cases
 
 
@@ -333,10 +365,14 @@ def main():
     DecGridRL, gridload = _load_reference()
     import contextlib
     import io
-    beam_tables()
-    handmade_data(gridload)
+    only = [a for a in sys.argv[1:] if not a.startswith("-")]
+    if not only:
+        beam_tables()
+        handmade_data(gridload)
     total = 0
     for case in build_cases(gridload):
+        if only and not any(case["name"].startswith(o) for o in only):
+            continue
         with contextlib.redirect_stdout(io.StringIO()):  # env.done() prints
             rec = run_case(DecGridRL, case)
         path = save_case(case, rec)

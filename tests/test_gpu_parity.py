@@ -55,6 +55,8 @@ def full_obs(env, obs, cfg):
     o = obs.cpu().numpy().astype(np.float64)
     if env.dist_obs is not None and not cfg.get("dijkstra_input"):
         o[:, :, 3] = env.dist_obs.cpu().numpy().astype(np.float64)
+    if env.minimap_obs is not None:  # the minimap overwrites layers 3 and 4
+        o[:, :, 3:5] = env.minimap_obs.cpu().numpy()
     return o
 
 
@@ -133,6 +135,19 @@ BATCH_CASES = {
     "dist_map_sharing": (base_cfg(numrobot=4, dist_reward=1, comm_radius=6, allow_comm=1, map_sharing=1,
                                   sensor_config={"num_lasers": 11, "range": 4}),
                          lambda rs: bern(rs, 30, 30, 0.15), 6, 30),
+    # minimap layers (mini_map_rad > 0): the template
+    # config's shape, down-scales with dist / dijkstra underneath, up-scale,
+    # equal sizes (cv::resize copies)
+    "minimap_ego5_mini10_comm": (base_cfg(numrobot=3, egoradius=5, mini_map_rad=10, comm_radius=10,
+                                          allow_comm=1, map_sharing=1, sensor_config={"num_lasers": 21, "range": 6}),
+                                 lambda rs: bern(rs, 40, 40, 0.15), 6, 30),
+    "minimap_dist_dijkstra": (base_cfg(numrobot=2, mini_map_rad=7, dist_reward=1, dijkstra_input=1,
+                                       sensor_config={"num_lasers": 11, "range": 4}),
+                              lambda rs: tri(rs, 30, 30), 6, 30),
+    "minimap_upscale": (base_cfg(numrobot=2, egoradius=4, mini_map_rad=2, sensor_type="square_sensor",
+                                 sensor_config={"range": 1}), lambda rs: bern(rs, 20, 20, 0.1), 6, 30),
+    "minimap_equal_sizes": (base_cfg(numrobot=2, egoradius=3, mini_map_rad=3), lambda rs: bern(rs, 24, 24, 0.1),
+                            4, 20),
 }
 
 
