@@ -63,6 +63,7 @@ struct SState {
   int B, N, W, L, G, RW, r, P;
   double pen, fpen, term, dincr;
   int dist, scan, maxsteps, auto_reset, grid_mode;
+  int abl;  // timing ablations (MARLCOV_SG_ABL, results invalid): 1 no sense, 2 no phase B, 4 no moves
   uint32_t mg_L;  // floor(i / L) == umulhi(i, mg_L) (L >= 2)
   uint64_t seed;
   const uint64_t* gneg;   // [G][W][RW] grid < 0
@@ -226,6 +227,12 @@ __global__ __launch_bounds__(256) void sg_reset_kernel(SState s, const uint8_t* 
 // --------------------------------------------------------------------------
 // SuperGridRL.step (:74-225), one wave per env, lane i = robot i.
 // --------------------------------------------------------------------------
+// R >= 0: senseradius R at compile time — the window of every plane around
+// the PRE-move cell, extended by the one cell a move can shift it, is loaded
+// in a single round together with the target's dist value, and the post-move
+// window comes from registers (one load round instead of one per window row,
+// twice).  R < 0: any radius, rows loaded as the loops reach them.
+template <int R>
 __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* __restrict__ actions,
                                                       const int32_t* __restrict__ quot,
                                                       double* __restrict__ reward,
@@ -235,7 +242,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = blockIdx.x * kEnvsPerBlock + w;
   if (e >= s.B) return;
-  const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = s.r;
+  const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = R >= 0 ? R : s.r;
   const bool me = lane < N;
   // every load that depends only on e is issued up front (one round trip)
   const int my_act = me ? (int)actions[(size_t)e * N + lane] : 255;  // slot `lane`'s action byte
@@ -280,12 +287,35 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     else if (u == 1) tx = x + 1;
     else if (u == 2) ty = y + 1;
     else if (u == 3) ty = y - 1;
-    const bool gfree = me && tx >= 0 && tx < W && ty >= 0 && ty < L && !bit_at(gneg, RW, tx, ty);
-    // pre-move distance_map[x, y] (:117-118, 139): the dist layer of the last state
+    const bool inb = me && tx >= 0 && tx < W && ty >= 0 && ty < L;
+    // pre-move distance_map[x, y] (:117-118, 139): the dist layer of the last
+    // state (loaded whether or not the move succeeds: no wait on the grid)
     double dv = 0.0;
-    if (s.dist && gfree && u < 4) dv = (double)s.dist_plane[((size_t)e * W + tx) * L + ty];
+    if (s.dist && inb && u < 4) dv = (double)s.dist_plane[((size_t)e * W + tx) * L + ty];
+    constexpr int NE = R >= 0 ? 2 * R + 3 : 1;  // extended window rows
+    constexpr int kRowUnroll = R >= 0 ? 2 * R + 1 : 1;
+    constexpr int kColUnroll = R >= 0 ? 2 * R + 1 : 1;
+    uint32_t xn[NE], xp[NE], xc[NE];             // bit b = cell y - R - 1 + b
+    bool gfree;
+    if constexpr (R >= 0) {
+      const int c0e = y - R - 1;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int j = x - R - 1 + k;
+        const bool ok = me && j >= 0 && j < W;
+        const size_t ro = (size_t)(ok ? j : 0) * RW;
+        xn[k] = ok ? row_field(gneg + ro, RW, c0e) : 0u;
+        xp[k] = ok ? row_field(gpos + ro, RW, c0e) : 0u;
+        xc[k] = ok ? row_field(cov + ro, RW, c0e) : 0u;
+      }
+      const int ddx = tx - x, ddy = ty - y;
+      const uint32_t trow = ddx < 0 ? xn[R] : (ddx > 0 ? xn[R + 2] : xn[R + 1]);
+      gfree = inb && !((trow >> (R + 1 + ddy)) & 1u);
+    } else {
+      gfree = inb && !bit_at(gneg, RW, tx, ty);
+    }
     double v = 0.0;
-    for (int k = 0; k < N; ++k) {  // slot order; robot z = the one with slot k
+    for (int k = 0; k < ((s.abl & 4) ? 0 : N); ++k) {  // slot order; robot z = the one with slot k
       const int z = s.scan ? (__ffsll((unsigned long long)__ballot(me && slot == k)) - 1) : k;
       const int zu = __shfl(u, z);
       if (zu >= 4) continue;  // not a move: nothing happens (no penalty)
@@ -315,26 +345,41 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     const int n = 2 * r + 1;
     const int c0 = y - r;
     const uint32_t vm = mask32(max(0, -c0), min(n, L - c0));
+    const int mdx = x - x_old, msh = 1 + (y - y_old);  // post-move window in the extended one
+    // window row jj of plane `a`: from the staged registers (R >= 0) or HBM
+    auto field = [&](const uint32_t* a, const uint64_t* plane, int jj, int j) -> uint32_t {
+      if constexpr (R >= 0) {
+        const uint32_t t = mdx < 0 ? a[jj] : (mdx > 0 ? a[jj + 2] : a[jj + 1]);
+        return (t >> msh) & vm;
+      } else {
+        return row_field(plane + (size_t)j * RW, RW, c0) & vm;
+      }
+    };
     int cnt = 0;
-    if (me) {
-      for (int jj = 0; jj < n; ++jj) {
+    if (me && !(s.abl & 1)) {
+#pragma unroll kRowUnroll
+      for (int jj = 0; jj < (R >= 0 ? 2 * R + 1 : n); ++jj) {
         const int j = x - r + jj;
         if (j < 0 || j >= W) continue;
-        const uint32_t fneg = row_field(gneg + (size_t)j * RW, RW, c0) & vm;
-        const uint32_t fpos = row_field(gpos + (size_t)j * RW, RW, c0) & vm;
-        const uint32_t fcov = row_field(cov + (size_t)j * RW, RW, c0) & vm;
+        const uint32_t fneg = field(xn, gneg, jj, j);
+        const uint32_t fpos = field(xp, gpos, jj, j);
+        const uint32_t fcov = field(xc, cov, jj, j);
         uint32_t lower = 0;
-        for (int m = 0; m < lane; ++m) {
+        for (int m = 0; m < N; ++m) {  // uniform trip count; robots m < lane count
           const int xm = s_x[w][m], ym = s_y[w][m];
-          if (abs(j - xm) <= r) lower |= mask32(max(0, ym - r - c0), min(n, ym + r + 1 - c0));
+          const uint32_t cm = mask32(max(0, ym - r - c0), min(n, ym + r + 1 - c0));
+          lower |= (m < lane && abs(j - xm) <= r) ? cm : 0u;
         }
         const uint32_t ge0 = vm & ~fneg;
         const uint32_t nw = ge0 & ~fcov & ~lower;
         cnt += __popc(nw);
-        for (uint32_t bits = ge0; bits; bits &= bits - 1) {
-          const int b = __ffs(bits) - 1;
-          if ((nw >> b) & 1u) v = v + (((fpos >> b) & 1u) ? 1.0 : 0.0);
-          else v = v - s.fpen;
+        // raster fold, branch-free: v - fpen == v + (-fpen) in IEEE
+        const double mfp = -s.fpen;
+#pragma unroll kColUnroll
+        for (int b = 0; b < (R >= 0 ? 2 * R + 1 : n); ++b) {
+          const double t = ((nw >> b) & 1u) ? (((fpos >> b) & 1u) ? 1.0 : 0.0) : mfp;
+          const double vt = v + t;
+          v = ((ge0 >> b) & 1u) ? vt : v;
         }
       }
     }
@@ -342,28 +387,37 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     // phase B: maps (idempotent ORs of the whole window) and state planes
     const size_t WL = (size_t)W * L;
     uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
-    if (me) {
+    if (me && !(s.abl & 2)) {
       uint8_t* pl_obst = pl + (size_t)s.P * WL;
       uint8_t* pl_free = pl + (size_t)(s.P + 1) * WL;
-      for (int jj = 0; jj < n; ++jj) {
+#pragma unroll kRowUnroll
+      for (int jj = 0; jj < (R >= 0 ? 2 * R + 1 : n); ++jj) {
         const int j = x - r + jj;
         if (j < 0 || j >= W) continue;
-        const uint32_t fneg = row_field(gneg + (size_t)j * RW, RW, c0) & vm;
+        const uint32_t fneg = field(xn, gneg, jj, j);
         const uint32_t ge0 = vm & ~fneg;
         or_field(cov + (size_t)j * RW, RW, c0, ge0);
         or_field(obst + (size_t)j * RW, RW, c0, fneg);
-        for (uint32_t bits = vm; bits; bits &= bits - 1) {
-          const int b = __ffs(bits) - 1;
-          const size_t cell = (size_t)j * L + (c0 + b);
-          if ((fneg >> b) & 1u) pl_obst[cell] = 1;
-          else pl_free[cell] = 0;
+        uint8_t* row_o = pl_obst + (size_t)j * L + c0;
+        uint8_t* row_f = pl_free + (size_t)j * L + c0;
+#pragma unroll kColUnroll
+        for (int b = 0; b < (R >= 0 ? 2 * R + 1 : n); ++b) {  // obstacle -> 1 in layer P, else 0 in _free
+          const bool ob = (fneg >> b) & 1u;
+          uint8_t* dst = (ob ? row_o : row_f) + b;
+          if ((vm >> b) & 1u) *dst = ob ? 1 : 0;
         }
       }
     }
+    // robot cells: clear the old one, set the new one.  With one shared layer
+    // (use_scanning) a cell vacated by one robot may be entered by another in
+    // the same step: that clear is skipped, so no store has to wait for
+    // another (robots are distinct, so each cell gets one store at most)
     const bool moved = me && (x != x_old || y != y_old);
     const size_t lay = (size_t)(s.scan ? 0 : lane) * WL;
-    if (moved) pl[lay + (size_t)x_old * L + y_old] = 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clears land before the sets
+    bool reoccupied = false;
+    if (s.scan)
+      for (int m = 0; m < N; ++m) reoccupied |= s_x[w][m] == x_old && s_y[w][m] == y_old;
+    if (moved && !reoccupied) pl[lay + (size_t)x_old * L + y_old] = 0;
     if (moved) pl[lay + (size_t)x * L + y] = 1;
 
     // motion_penalty(a) on every slot (:203-208, 227-243): a is the quotient
@@ -804,6 +858,10 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   s.auto_reset = c.auto_reset != 0;
   s.grid_mode = c.reset_grid_mode;
   s.mg_L = mc::magic_div((uint32_t)c.length);
+  {
+    const char* ab = getenv("MARLCOV_SG_ABL");
+    s.abl = ab ? atoi(ab) : 0;
+  }
   s.seed = c.seed;
   // distance planes: u16 rows with an odd dword pitch (the row pass writes
   // column v of W rows at once: distinct banks)
@@ -959,8 +1017,20 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   SG_TRY(hipSetDevice(E->device));
   if (E->stale) SG_TRY(launch_dist(E, st));  // the pre-move distance_map of the current maps
   const int blocks = (E->s.B + mcs::kEnvsPerBlock - 1) / mcs::kEnvsPerBlock;
-  hipLaunchKernelGGL(mcs::sg_step_kernel, dim3(blocks), dim3(64 * mcs::kEnvsPerBlock), 0, st, E->s,
-                     dev_actions, dev_quot, dev_reward, dev_done);
+  auto kern = mcs::sg_step_kernel<-1>;
+  switch (E->s.r) {  // compile-time radii of the reference configs (staged window)
+    case 1: kern = mcs::sg_step_kernel<1>; break;
+    case 2: kern = mcs::sg_step_kernel<2>; break;
+    case 3: kern = mcs::sg_step_kernel<3>; break;
+    default: break;
+  }
+  static const bool force_generic = [] {  // MARLCOV_SG_GENERIC=1: A/B against the runtime-radius kernel
+    const char* v = getenv("MARLCOV_SG_GENERIC");
+    return v && atoi(v) == 1;
+  }();
+  if (force_generic) kern = mcs::sg_step_kernel<-1>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * mcs::kEnvsPerBlock), 0, st, E->s, dev_actions, dev_quot,
+                     dev_reward, dev_done);
   SG_TRY(hipGetLastError());
   SG_TRY(launch_dist(E, st));
   E->stale = false;
