@@ -63,6 +63,8 @@ struct SState {
   int B, N, W, L, G, RW, r, P;
   double pen, fpen, term, dincr;
   int dist, scan, maxsteps, auto_reset, grid_mode;
+  int dist_full;   // MARLCOV_SG_FULL_DIST=1: rewrite the whole distance layer every step
+  int32_t* dist_M; // [B] max(d) of the layer as last written (-1 unknown, -2 no source)
   int abl;  // timing ablations (MARLCOV_SG_ABL, results invalid): 1 no sense, 2 no phase B, 4 no moves
   uint32_t mg_L;  // floor(i / L) == umulhi(i, mg_L) (L >= 2)
   uint64_t seed;
@@ -508,7 +510,9 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
   const int W = s.W, L = s.L, RW = s.RW;
   const int nw = W * RW;
   const size_t WL = (size_t)W * L;
-  if (s.full[e]) write_full_layers(s, e, tid, NT, s_px, s_py);
+  const bool was_full = s.full[e] != 0;  // read by every thread before it is cleared
+  const int M_old = s.dist_M[e];
+  if (was_full) write_full_layers(s, e, tid, NT, s_px, s_py);
   uint64_t* cur = reinterpret_cast<uint64_t*>(smem);
   uint64_t* nxt = cur + nw;
   uint8_t* d8 = reinterpret_cast<uint8_t*>(nxt + nw);
@@ -530,6 +534,7 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
   float* out = s.dist_plane + (size_t)e * WL;
   if (!any_src) {  // no source cell: SciPy's -1 everywhere -> 1 - (-1)
     for (size_t i = tid; i < WL; i += NT) out[i] = 2.0f;
+    if (tid == 0) s.dist_M[e] = -2;
     return;
   }
   int M = 0;
@@ -565,8 +570,28 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
   }
   const float Mf = (float)M;
   for (int d = tid; d <= M; d += NT) lut[d] = dist_value((float)d, Mf);
+  if (tid == 0) s.dist_M[e] = M;
+  // Since the layer was last written only this step's sensing changed the
+  // map: newly covered cells n lie in the robots' windows (|n - p_i| <= r,
+  // Chebyshev), and a cell's d changes only if its nearest source was such a
+  // cell, i.e. |c - n|_1 <= d_old(c) <= M_old.  So with max(d) unchanged every
+  // changed value lies within r + M_old of a robot, and the rest of the layer
+  // already holds the exact new values.  A changed max, a full-rewrite flag
+  // (reset / state upload) or MARLCOV_SG_FULL_DIST rewrites the whole layer.
+  const int h = s.r + (M_old > 0 ? M_old : 0) + 1, side = 2 * h + 1;
+  const bool all = was_full || s.dist_full || M != M_old || M_old < 0 ||
+                   (size_t)s.N * side * side >= WL;
   __syncthreads();
-  if ((L & 3) == 0) {
+  if (!all) {
+    const int per = side * side;
+    for (int idx = tid; idx < s.N * per; idx += NT) {
+      const int i = idx / per, rem = idx - i * per;
+      const int rr = rem / side, cc = rem - rr * side;
+      const int u = s.pos[((size_t)e * s.N + i) * 2] - h + rr;
+      const int v = s.pos[((size_t)e * s.N + i) * 2 + 1] - h + cc;
+      if (u >= 0 && u < W && v >= 0 && v < L) out[(size_t)u * L + v] = lut[d8[(size_t)u * L + v]];
+    }
+  } else if ((L & 3) == 0) {
     const uint32_t* d4 = reinterpret_cast<const uint32_t*>(d8);
     float4* o4 = reinterpret_cast<float4*>(out);
     for (size_t g = tid; g < WL / 4; g += NT) {
@@ -861,6 +886,8 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   {
     const char* ab = getenv("MARLCOV_SG_ABL");
     s.abl = ab ? atoi(ab) : 0;
+    const char* fd = getenv("MARLCOV_SG_FULL_DIST");
+    s.dist_full = fd && atoi(fd) == 1;
   }
   s.seed = c.seed;
   // distance planes: u16 rows with an odd dword pitch (the row pass writes
@@ -896,6 +923,7 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   SG_ALLOC(a_prev, int32_t*, B * 4);
   SG_ALLOC(episode, uint32_t*, B * 4);
   SG_ALLOC(full, uint8_t*, B);
+  SG_ALLOC(dist_M, int32_t*, B * 4);
   SG_ALLOC(err, uint32_t*, 4);
   if (!E->lds) {
     SG_ALLOC(scratch, uint16_t*, B * s.W * E->pitch * 2);
@@ -910,6 +938,7 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
     if (he == hipSuccess) he = hipMemcpy(s.a_prev, ap.data(), B * 4, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(s.done_thresh, dt.data(), B * 8, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(s.full, fl.data(), B, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemset(s.dist_M, 0xFF, B * 4);
     if (he != hipSuccess) {
       mc_sg_destroy(E);
       return sg_fail(MC_EHIP, "mc_sg_create: %s", hipGetErrorString(he));
@@ -949,6 +978,7 @@ int mc_sg_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void*
   hipLaunchKernelGGL(mcs::sg_pack_kernel, dim3(blocks), dim3(256), 0, st, E->s, dev_grids,
                      (uint64_t*)E->s.gneg, (uint64_t*)E->s.gpos, (int32_t*)E->s.numpos);
   SG_TRY(hipGetLastError());
+  SG_TRY(hipMemsetAsync(E->s.full, 1, (size_t)E->s.B, st));  // new obstacles: every layer value may change
   E->stale = true;
   return check_numpos(E, st);
 }
@@ -966,6 +996,7 @@ int mc_sg_generate_grids(void* env, uint64_t seed, double p_obst, void* stream) 
   hipLaunchKernelGGL(mcs::sg_gen_kernel, dim3(blocks), dim3(256), 0, st, E->s, seed, thresh,
                      (uint64_t*)E->s.gneg, (uint64_t*)E->s.gpos, (int32_t*)E->s.numpos);
   SG_TRY(hipGetLastError());
+  SG_TRY(hipMemsetAsync(E->s.full, 1, (size_t)E->s.B, st));  // new obstacles: every layer value may change
   E->stale = true;
   return check_numpos(E, st);
 }
@@ -976,6 +1007,7 @@ int mc_sg_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {
   SG_TRY(hipSetDevice(E->device));
   SG_TRY(hipMemcpyAsync(E->s.env_grid, dev_env_grid, (size_t)E->s.B * 4, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream));
+  SG_TRY(hipMemsetAsync(E->s.full, 1, (size_t)E->s.B, (hipStream_t)stream));
   E->stale = true;
   return MC_OK;
 }
