@@ -269,7 +269,9 @@ enum {
   MC_SG_FIELD_NUMPOS = 9,     /* int32  [G] count_nonzero(grid > 0)           */
   MC_SG_FIELD_GRID_NEG = 10,  /* uint64 [G][W][RW] grid < 0                   */
   MC_SG_FIELD_GRID_POS = 11,  /* uint64 [G][W][RW] grid > 0                   */
-  MC_SG_FIELD_COUNT = 12
+  MC_SG_FIELD_EP_PC = 12,     /* double [B] percent_covered() at the last done (read-only) */
+  MC_SG_FIELD_EP_LEN = 13,    /* int32  [B] _currstep at the last done (read-only) */
+  MC_SG_FIELD_COUNT = 14
 };
 
 /* Replaces SuperGridRL.__init__ (:27-72) minus the first reset. */

@@ -111,7 +111,7 @@ class McSgLayout(ctypes.Structure):
 
 (SG_FIELD_POS, SG_FIELD_COVERED, SG_FIELD_OBST, SG_FIELD_COV_COUNT, SG_FIELD_CURRSTEP,
  SG_FIELD_DONE_THRESH, SG_FIELD_A_PREV, SG_FIELD_ENV_GRID, SG_FIELD_EPISODE, SG_FIELD_NUMPOS,
- SG_FIELD_GRID_NEG, SG_FIELD_GRID_POS) = range(12)
+ SG_FIELD_GRID_NEG, SG_FIELD_GRID_POS, SG_FIELD_EP_PC, SG_FIELD_EP_LEN) = range(14)
 
 
 # (name, restype, argtypes) for every symbol include/marlcov.h declares

@@ -65,6 +65,8 @@ struct SState {
   int dist, scan, maxsteps, auto_reset, grid_mode;
   int dist_full;   // MARLCOV_SG_FULL_DIST=1: rewrite the whole distance layer every step
   int32_t* dist_M; // [B] max(d) of the layer as last written (-1 unknown, -2 no source)
+  double* ep_pc;   // [B] episode record at done (before an auto-reset): percent_covered()
+  int32_t* ep_len; // [B] ... and _currstep
   int abl;  // timing ablations (MARLCOV_SG_ABL, results invalid): 1 no sense, 2 no phase B, 4 no moves
   uint32_t mg_L;  // floor(i / L) == umulhi(i, mg_L) (L >= 2)
   uint64_t seed;
@@ -261,6 +263,8 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     if (lane == 0) {
       reward[e] = 0.0;
       done[e] = 1;
+      s.ep_pc[e] = (double)cc0 / (double)npos;
+      s.ep_len[e] = cs0;
     }
   } else {
     const size_t mw = (size_t)W * RW;
@@ -448,6 +452,10 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
       s.cov_cnt[e] = cc;
       reward[e] = total;
       done[e] = (uint8_t)dn;
+      if (dn) {  // the episode record (Utils/utils.py:138-141)
+        s.ep_pc[e] = pc;
+        s.ep_len[e] = cs;
+      }
     }
     is_done = __shfl(dn, 0) != 0;
   }
@@ -807,6 +815,8 @@ SgField sg_field(SgEnv* E, int f) {
     case MC_SG_FIELD_NUMPOS: return {(void*)s.numpos, G * 4};
     case MC_SG_FIELD_GRID_NEG: return {(void*)s.gneg, G * mw * 8};
     case MC_SG_FIELD_GRID_POS: return {(void*)s.gpos, G * mw * 8};
+    case MC_SG_FIELD_EP_PC: return {s.ep_pc, B * 8};
+    case MC_SG_FIELD_EP_LEN: return {s.ep_len, B * 4};
     default: return {nullptr, -1};
   }
 }
@@ -924,6 +934,8 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   SG_ALLOC(episode, uint32_t*, B * 4);
   SG_ALLOC(full, uint8_t*, B);
   SG_ALLOC(dist_M, int32_t*, B * 4);
+  SG_ALLOC(ep_pc, double*, B * 8);
+  SG_ALLOC(ep_len, int32_t*, B * 4);
   SG_ALLOC(err, uint32_t*, 4);
   if (!E->lds) {
     SG_ALLOC(scratch, uint16_t*, B * s.W * E->pitch * 2);
@@ -1093,6 +1105,7 @@ int mc_sg_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, vo
   if (!E || !dev_src) return sg_fail(MC_EINVAL, "mc_sg_set_state: null argument");
   SgField d = sg_field(E, f);
   if (!d.ptr) return sg_fail(MC_EINVAL, "unknown state field %d", f);
+  if (f == MC_SG_FIELD_EP_PC || f == MC_SG_FIELD_EP_LEN) return sg_fail(MC_EINVAL, "field %d is read-only", f);
   if (bytes != d.bytes) return sg_fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   hipStream_t st = (hipStream_t)stream;
   SG_TRY(hipSetDevice(E->device));

@@ -42,8 +42,16 @@ def random_policy(env, seed=0):
     return pi
 
 
+def _record_fields(env):
+    """(get_state function, episode-record fields) of a batch env type."""
+    if hasattr(env, "planes"):  # BatchSuperGridEnv
+        return env.lib.mc_sg_get_state, (_lib.SG_FIELD_EP_PC, _lib.SG_FIELD_EP_LEN)
+    return env.lib.mc_get_state, (_lib.FIELD_EP_PC, _lib.FIELD_EP_LEN)
+
+
 def generate_episodes(env, policy, episodes_per_env, max_steps=None, on_step=None, check_every=16):
-    """Run every env of ``env`` (a BatchCoverageEnv with auto_reset) until it
+    """Run every env of ``env`` (a BatchCoverageEnv or BatchSuperGridEnv with
+    auto_reset) until it
     finished ``episodes_per_env`` episodes.  ``policy(obs) -> uint8 [B, N]``
     device actions (255 in agent 0 = the sentinel, which ends the episode as
     in generate_episode).  ``on_step(t, actions, reward, done)`` is called
@@ -55,7 +63,7 @@ def generate_episodes(env, policy, episodes_per_env, max_steps=None, on_step=Non
     Envs that finish early keep running (a batch steps every env) but record
     nothing more."""
     if not env._cfg.auto_reset:
-        raise ValueError("generate_episodes needs a BatchCoverageEnv with auto_reset=True")
+        raise ValueError("generate_episodes needs a batch env with auto_reset=True")
     torch = env._torch
     B, E = env.num_envs, int(episodes_per_env)
     dev = env.device
@@ -67,15 +75,19 @@ def generate_episodes(env, policy, episodes_per_env, max_steps=None, on_step=Non
     ep_pc = torch.empty(B, dtype=torch.float64, device=dev)
     ep_len = torch.empty(B, dtype=torch.int32, device=dev)
     rows = torch.arange(B, device=dev)
-    obs = env.obs if env.adj is None else (env.obs, env.adj)
+    get_state, (f_pc, f_len) = _record_fields(env)
+    if hasattr(env, "planes"):
+        obs = (env.planes, env.dist)
+    else:
+        obs = env.obs if env.adj is None else (env.obs, env.adj)
     t = 0
     while True:
         actions = policy(obs)
         obs, reward, done = env.step(actions)
         ret += reward
-        for field, buf in ((_lib.FIELD_EP_PC, ep_pc), (_lib.FIELD_EP_LEN, ep_len)):
-            _lib.check(env.lib.mc_get_state(env._h, field, buf.data_ptr(), buf.numel() * buf.element_size(),
-                                            env._stream()), "mc_get_state")
+        for field, buf in ((f_pc, ep_pc), (f_len, ep_len)):
+            _lib.check(get_state(env._h, field, buf.data_ptr(), buf.numel() * buf.element_size(),
+                                 env._stream()), "get_state")
         d = done.bool()
         take = d & (count < E)
         idx = count.clamp(max=E - 1)

@@ -24,6 +24,7 @@ _SG_DTYPES = {
     _lib.SG_FIELD_DONE_THRESH: "float64", _lib.SG_FIELD_A_PREV: "int32",
     _lib.SG_FIELD_ENV_GRID: "int32", _lib.SG_FIELD_EPISODE: "int32", _lib.SG_FIELD_NUMPOS: "int32",
     _lib.SG_FIELD_GRID_NEG: "int64", _lib.SG_FIELD_GRID_POS: "int64",
+    _lib.SG_FIELD_EP_PC: "float64", _lib.SG_FIELD_EP_LEN: "int32",
 }
 
 
@@ -200,6 +201,7 @@ class BatchSuperGridEnv:
             _lib.SG_FIELD_COV_COUNT: (B,), _lib.SG_FIELD_CURRSTEP: (B,), _lib.SG_FIELD_DONE_THRESH: (B,),
             _lib.SG_FIELD_A_PREV: (B,), _lib.SG_FIELD_ENV_GRID: (B,), _lib.SG_FIELD_EPISODE: (B,),
             _lib.SG_FIELD_NUMPOS: (G,), _lib.SG_FIELD_GRID_NEG: (G, W, RW), _lib.SG_FIELD_GRID_POS: (G, W, RW),
+            _lib.SG_FIELD_EP_PC: (B,), _lib.SG_FIELD_EP_LEN: (B,),
         }[field]
 
     def get_state(self, field):

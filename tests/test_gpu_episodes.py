@@ -86,3 +86,53 @@ def test_batched_test_RLalg_statistics(torch_cuda):
     assert 0.0 < avg <= 100.0
     # a 30-step episode of 1 robot with a 3x3 sensor cannot cover a 15x15 grid
     assert all(-5 * 30 <= r <= 9 * 30 for r in rewards)
+
+
+def test_generate_episodes_super_matches_oracle_loop(torch_cuda):
+    """The same driver over BatchSuperGridEnv (grid_rl_main.py can run either
+    env): per-episode return, length and percent_covered() vs the oracle."""
+    import marlcov
+    from marlcov import _lib
+    from marlcov.episodes import generate_episodes, random_policy
+    from marlcov.super_env import decode_super_action  # noqa: F401  (API surface)
+    from oracle.super_ref import SuperGridRLRef
+    torch = torch_cuda
+    c = dict(numrobot=3, train_maxsteps=1000, test_maxsteps=1000, collision_penalty=5, senseradius=1,
+             free_penalty=0.2, done_thresh=0.5, done_incr=0.1, terminal_reward=30, dist_reward=1,
+             use_scanning=1)
+    rs = np.random.RandomState(21)
+    B, E, cut = 8, 3, 16
+    grids = [rs.choice([1.0, -1.0], size=(12, 14), p=[0.85, 0.15]) for _ in range(B)]
+    env = marlcov.BatchSuperGridEnv(c, B, grids=grids, auto_reset=True, maxsteps=cut, seed=3)
+    env.reset()
+    pos = env.get_state(_lib.SG_FIELD_POS).cpu().numpy()
+    refs = []
+    for b in range(B):
+        np.random.seed(b)
+        r = SuperGridRLRef([grids[b]], c)
+        r.reset(False, None, positions=pos[b])
+        refs.append(r)
+    episodes = [[] for _ in range(B)]
+    acc = np.zeros(B)
+    base = random_policy(env, seed=8)
+
+    def on_step(t, actions, reward, done):
+        acts = actions.cpu().numpy()
+        rew, dn = reward.cpu().numpy(), done.cpu().numpy()
+        p = env.get_state(_lib.SG_FIELD_POS).cpu().numpy()
+        for b in range(B):
+            _, r, d = refs[b].step(int(sum(int(x) * 4 ** i for i, x in enumerate(acts[b]))))
+            d = d or refs[b]._currstep == cut
+            assert float(r) == rew[b] and bool(d) == bool(dn[b]), (t, b)
+            acc[b] += r
+            if d:
+                episodes[b].append((acc[b], refs[b]._currstep, refs[b].percent_covered()))
+                acc[b] = 0.0
+                refs[b].reset(False, None, positions=p[b])
+
+    out = generate_episodes(env, base, E, max_steps=1000, on_step=on_step)
+    for b in range(B):
+        for k in range(E):
+            r, n, pc = episodes[b][k]
+            assert out["reward"][b, k] == r and out["length"][b, k] == n, (b, k)
+            assert out["percent_covered"][b, k] == pc, (b, k)
