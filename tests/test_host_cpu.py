@@ -210,3 +210,31 @@ def test_super_create_rejects_bad_config(lib):
         setattr(cc, field, bad)
         assert lib.mc_sg_create(ctypes.byref(cc), 0, ctypes.byref(h)) == _lib.MC_EINVAL
         assert lib.mc_last_error()
+
+
+def test_gridload_png_semantics(tmp_path):
+    """Utils/gridmaker.py:82-104: PNG maps -> clip(img - 1, -1, 1) as float64,
+    at most numgrids files in os.listdir order, half/half split with the
+    len // 2 == 1 quirk (both sets = every map; one map: empty train set)."""
+    from PIL import Image
+    from marlcov import gridload
+    rs = np.random.RandomState(3)
+    imgs = {}
+    for i in range(5):
+        img = rs.choice(np.array([0, 1, 2, 255], dtype=np.uint8), size=(9, 11))
+        name = f"map{i}.png"
+        Image.fromarray(img, mode="L").save(tmp_path / name)
+        imgs[name] = np.clip(img.astype(float) - 1, -1, 1)
+    cfg = {"grid_dir": str(tmp_path), "numgrids": 4}
+    train, test = gridload(cfg, sort=True)
+    names = sorted(imgs)[:4]
+    assert len(train) == 2 and len(test) == 2
+    for g, n in zip(train + test, names):
+        assert g.dtype == np.float64 and set(np.unique(g)) <= {-1.0, 0.0, 1.0}
+        np.testing.assert_array_equal(g, imgs[n])
+    tr, te = gridload({"grid_dir": str(tmp_path), "numgrids": 3}, sort=True)
+    assert len(tr) == 3 and len(te) == 3          # 3 // 2 == 1: both sets are every map
+    tr, te = gridload({"grid_dir": str(tmp_path), "numgrids": 1}, sort=True)
+    assert len(tr) == 0 and len(te) == 1          # 1 // 2 == 0: the reference's empty train set
+    tr, te = gridload({"grid_dir": str(tmp_path), "numgrids": 10})  # filesystem order, all 5
+    assert len(tr) == 2 and len(te) == 3
