@@ -180,7 +180,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
-    ap.add_argument("--cpu-procs", type=int, default=8)
+    # the GPU box's host share is 16 CPUs per GPU (os.cpu_count() there shows
+    # the whole machine): one single-env oracle process per core
+    ap.add_argument("--cpu-procs", type=int, default=16)
     ap.add_argument("--cpu-secs", type=float, default=2.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--maxsteps", type=int, default=None,
