@@ -369,3 +369,40 @@ def test_determinism_same_seed(torch_cuda):
         outs.append(acc)
     for (o1, r1, d1), (o2, r2, d2) in zip(*outs):
         assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2)
+
+
+# ---------------------------------------------------------------------------
+# reset_grid_mode="random": an auto-reset draws a new grid from the pool; the
+# new episode equals an oracle reset on that grid at the device-drawn cells
+# ---------------------------------------------------------------------------
+def test_auto_reset_random_grid_pool(torch_cuda):
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=2, maxsteps=5, sensor_config={"num_lasers": 9, "range": 4})
+    rs = np.random.RandomState(31)
+    pool = [bern(rs, 20, 20, 0.2) for _ in range(5)]
+    B = 12
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=pool, auto_reset=True, seed=17, reset_grid_mode="random")
+    env.reset()
+    st = device_state(env)
+    refs = [oracle_from_device(st, b, cfg) for b in range(B)]
+    used = set()
+    for t in range(30):
+        acts = rs.randint(0, 4, size=(B, 2)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), (t, b)
+            if d:  # a fresh oracle on the grid the device drew, reset at its cells
+                g = int(st["env_grid"][b])
+                assert 0 <= g < len(pool)
+                used.add(g)
+                np.random.seed(0)
+                refs[b] = DecGridRLRef([pool[g]], cfg)
+                o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in st["pos"][b]])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=f"t={t} env {b}")
+            compare_env(st, b, refs[b], f"t={t} env {b}")
+    assert len(used) >= 4  # the draws cover the pool
+    env.check()

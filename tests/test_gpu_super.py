@@ -266,3 +266,46 @@ def test_super_bench_workload_full_size(torch_cuda):
                 r.reset(False, None, positions=st["pos"][b])
             compare(st, b, r, f"full-size step {t} env {b}")
     env.check()
+
+
+def test_super_auto_reset_random_grid_pool(torch_cuda):
+    """reset_grid_mode="random": every auto-reset lands on the pool grid the
+    device drew; the new episode equals an oracle reset there."""
+    import marlcov
+    torch = torch_cuda
+    cfg = sg_cfg(numrobot=2, senseradius=1, dist_reward=1)
+    rs = np.random.RandomState(41)
+    pool = [bernoulli(rs, 14, 18, 0.2) for _ in range(5)]
+    B, cut = 10, 6
+    env = marlcov.BatchSuperGridEnv(cfg, B, grids=pool, auto_reset=True, maxsteps=cut, seed=23,
+                                    reset_grid_mode="random")
+    env.reset()  # every reset draws its grid in this mode, the first one too
+    st = device_state(env)
+    refs = []
+    for b in range(B):
+        np.random.seed(b)
+        r = SuperGridRLRef([pool[int(st["env_grid"][b])]], cfg)
+        r.reset(False, None, positions=st["pos"][b])
+        refs.append(r)
+        compare(st, b, r, f"random-grid reset env {b}")
+    used = set(int(g) for g in st["env_grid"])
+    for t in range(36):
+        digits = rs.randint(0, 4, size=(B, 2)).astype(np.uint8)
+        (_, _), rew, dn = env.step(torch.from_numpy(digits).cuda())
+        rew, dn = rew.cpu().numpy(), dn.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            _, rr, rd = refs[b].step(int(digits[b, 0]) + 4 * int(digits[b, 1]))
+            rd = rd or refs[b]._currstep == cut
+            assert float(rr) == rew[b] and bool(rd) == bool(dn[b]), (t, b)
+            if dn[b]:
+                g = int(st["env_grid"][b])
+                used.add(g)
+                a_prev, dt = refs[b].a_prev, refs[b]._done_thresh  # kept across resets
+                np.random.seed(0)
+                refs[b] = SuperGridRLRef([pool[g]], cfg)
+                refs[b].a_prev, refs[b]._done_thresh = a_prev, dt
+                refs[b].reset(False, None, positions=st["pos"][b])
+            compare(st, b, refs[b], f"random-grid step {t} env {b}")
+    assert len(used) >= 4
+    env.check()
