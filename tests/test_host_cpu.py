@@ -238,3 +238,16 @@ def test_gridload_png_semantics(tmp_path):
     assert len(tr) == 0 and len(te) == 1          # 1 // 2 == 0: the reference's empty train set
     tr, te = gridload({"grid_dir": str(tmp_path), "numgrids": 10})  # filesystem order, all 5
     assert len(tr) == 2 and len(te) == 3
+
+
+def test_episode_config_cut():
+    """marlcov.episodes.episode_config folds generate_episode's cut
+    (utils.py:25-28: _currstep == test/train maxsteps) into the env's maxsteps
+    (DecGridRL.done, dec_grid_rl.py:544): the smaller one ends the episode."""
+    from marlcov.episodes import episode_config
+    c = dict(maxsteps=1000, train_maxsteps=300, test_maxsteps=50)
+    assert episode_config(c, testing=True)["maxsteps"] == 50
+    assert episode_config(c, testing=False)["maxsteps"] == 300
+    c = dict(maxsteps=20, train_maxsteps=300, test_maxsteps=50)
+    assert episode_config(c, testing=True)["maxsteps"] == 20
+    assert c["maxsteps"] == 20  # the caller's dict is not modified
