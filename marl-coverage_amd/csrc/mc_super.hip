@@ -520,6 +520,10 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
   const size_t WL = (size_t)W * L;
   const bool was_full = s.full[e] != 0;  // read by every thread before it is cleared
   const int M_old = s.dist_M[e];
+  if (tid < s.N) {  // robot cells (the region writes below), loaded while the map loads
+    s_px[tid] = s.pos[((size_t)e * s.N + tid) * 2];
+    s_py[tid] = s.pos[((size_t)e * s.N + tid) * 2 + 1];
+  }
   if (was_full) write_full_layers(s, e, tid, NT, s_px, s_py);
   uint64_t* cur = reinterpret_cast<uint64_t*>(smem);
   uint64_t* nxt = cur + nw;
@@ -595,8 +599,8 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
     for (int idx = tid; idx < s.N * per; idx += NT) {
       const int i = idx / per, rem = idx - i * per;
       const int rr = rem / side, cc = rem - rr * side;
-      const int u = s.pos[((size_t)e * s.N + i) * 2] - h + rr;
-      const int v = s.pos[((size_t)e * s.N + i) * 2 + 1] - h + cc;
+      const int u = s_px[i] - h + rr;
+      const int v = s_py[i] - h + cc;
       if (u >= 0 && u < W && v >= 0 && v < L) out[(size_t)u * L + v] = lut[d8[(size_t)u * L + v]];
     }
   } else if ((L & 3) == 0) {
