@@ -595,13 +595,25 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
                    (size_t)s.N * side * side >= WL;
   __syncthreads();
   if (!all) {
+    // idx = (i * side + rr) * side + cc, divided once and then advanced by NT
+    // with carries (each digit step is < side, so one subtraction each)
     const int per = side * side;
+    const int q_nt = NT / side, st_cc = NT - q_nt * side;
+    const int st_i = q_nt / side, st_rr = q_nt - st_i * side;
+    int i = tid / per;
+    int rr = (tid - i * per) / side;
+    int cc = tid - i * per - rr * side;
     for (int idx = tid; idx < s.N * per; idx += NT) {
-      const int i = idx / per, rem = idx - i * per;
-      const int rr = rem / side, cc = rem - rr * side;
       const int u = s_px[i] - h + rr;
       const int v = s_py[i] - h + cc;
       if (u >= 0 && u < W && v >= 0 && v < L) out[(size_t)u * L + v] = lut[d8[(size_t)u * L + v]];
+      cc += st_cc;
+      int c = cc >= side;
+      cc -= c ? side : 0;
+      rr += st_rr + c;
+      c = rr >= side;
+      rr -= c ? side : 0;
+      i += st_i + c;
     }
   } else if ((L & 3) == 0) {
     const uint32_t* d4 = reinterpret_cast<const uint32_t*>(d8);
