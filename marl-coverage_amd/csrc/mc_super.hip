@@ -551,10 +551,13 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
   }
   int M = 0;
   if (any_cov) {
+    // word i = u * RW + w: divided once per thread, then advanced by NT with a carry
+    const int u0 = tid / RW, w0 = tid - u0 * RW;
+    const int st_u = NT / RW, st_w = NT - st_u * RW;
     for (int k = 0;; ++k) {
       int nz = 0;
+      int u = u0, w = w0;
       for (int i = tid; i < nw; i += NT) {
-        const int u = i / RW, w = i - u * RW;
         const uint64_t inval = (w == RW - 1) ? inval_last : 0ull;
         const uint64_t c = cur[i];
         const uint64_t up = u > 0 ? cur[i - RW] : ~0ull;
@@ -570,6 +573,10 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
           for (; leave; leave &= leave - 1) row[__ffsll((unsigned long long)leave) - 1] = dk;
         }
         nz |= (n & ~inval) != 0ull;
+        w += st_w;
+        const int cw = w >= RW;
+        w -= cw ? RW : 0;
+        u += st_u + cw;
       }
       if (!__syncthreads_or(nz)) {
         M = k + 1;
