@@ -402,7 +402,12 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
         if (j < 0 || j >= W) continue;
         const uint32_t fneg = field(xn, gneg, jj, j);
         const uint32_t ge0 = vm & ~fneg;
-        or_field(cov + (size_t)j * RW, RW, c0, ge0);
+        // staged window: OR only the bits not covered before this step (covered
+        // bits are cleared only by the reset below), so re-sensed rows cost no atomic
+        if constexpr (R >= 0)
+          or_field(cov + (size_t)j * RW, RW, c0, ge0 & ~field(xc, cov, jj, j));
+        else
+          or_field(cov + (size_t)j * RW, RW, c0, ge0);
         or_field(obst + (size_t)j * RW, RW, c0, fneg);
         uint8_t* row_o = pl_obst + (size_t)j * L + c0;
         uint8_t* row_f = pl_free + (size_t)j * L + c0;
