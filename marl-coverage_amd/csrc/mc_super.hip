@@ -411,11 +411,16 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
         or_field(obst + (size_t)j * RW, RW, c0, fneg);
         uint8_t* row_o = pl_obst + (size_t)j * L + c0;
         uint8_t* row_f = pl_free + (size_t)j * L + c0;
+        // staged window: a cell covered before this step already holds 0 in
+        // _free (the layers track the bitboards, and a full rewrite follows any
+        // reset / upload), so only new cells and obstacles are stored
+        uint32_t st = vm;
+        if constexpr (R >= 0) st = (ge0 & ~field(xc, cov, jj, j)) | fneg;
 #pragma unroll kColUnroll
         for (int b = 0; b < (R >= 0 ? 2 * R + 1 : n); ++b) {  // obstacle -> 1 in layer P, else 0 in _free
           const bool ob = (fneg >> b) & 1u;
           uint8_t* dst = (ob ? row_o : row_f) + b;
-          if ((vm >> b) & 1u) *dst = ob ? 1 : 0;
+          if ((st >> b) & 1u) *dst = ob ? 1 : 0;
         }
       }
     }
