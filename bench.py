@@ -187,9 +187,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--maxsteps", type=int, default=None,
                     help="episode length (auto-reset on done); default: the config's (1000, C5 2000)")
-    ap.add_argument("--eager", action="store_true", help="plain launches + per-launch events (no hipGraph)")
-    ap.add_argument("--graph-chunk", type=int, default=100, help="steps captured per hipGraph")
+    ap.add_argument("--launch", default="stream", choices=["stream", "graph", "events"],
+                    help="stream: K back-to-back launches; graph: uploaded hipGraph replay; "
+                         "events: per-launch HIP events")
+    ap.add_argument("--eager", action="store_true", help="alias of --launch events")
     args = ap.parse_args()
+    if args.eager:
+        args.launch = "events"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -242,53 +246,8 @@ def main():
     torch.cuda.synchronize(dev)
     env.check()
 
-    graphs = []
-    if not args.eager:
-        # K launches captured into hipGraphs (one per chunk of steps, each step
-        # reading its own action slice): the timed region replays them, so
-        # host launch overhead does not gate the GPU.  The kernel, its inputs
-        # and its work per step are unchanged.
-        chunk = max(1, min(args.graph_chunk, K))
-        for c0 in range(0, K, chunk):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                cs = torch.cuda.current_stream(dev).cuda_stream
-                for i in range(c0, min(K, c0 + chunk)):
-                    env.step_raw(actions[W + i].data_ptr(), rp, dp, op, cs)
-            graphs.append(g)
-        torch.cuda.synchronize(dev)
-
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if args.eager:
-        starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-        ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    if args.eager:
-        for i in range(K):
-            starts[i].record(stream)
-            env.step_raw(actions[W + i].data_ptr(), rp, dp, op, sp)
-            ends[i].record(stream)
-    else:
-        for g in graphs:
-            g.replay()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    if args.eager:
-        kern_ms = sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K
-    else:
-        # HIP events on the launch stream around the replayed launches: the
-        # average includes the kernel boundaries, so it bounds the kernel
-        # duration from above (rocprofv3 in profiles/ gives the bare kernel)
-        kern_ms = ev0.elapsed_time(ev1) / K
+    elapsed, kern_ms = timed_launches(lambda i, st: env.step_raw(actions[W + i].data_ptr(), rp, dp, op, st),
+                                      dev, K, args.launch)
     env.check()
     listed = None
     if dr:  # maps the last step sent to the full distance transform (diagnostic)
@@ -324,14 +283,13 @@ def main():
         "dtype": "f64+u64",
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
-                   "launch": "eager" if args.eager else "hipGraph replay",
+                   "launch": LAUNCH_DESC[args.launch],
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
                    **({"dist_full_transforms_last_step": listed} if dr else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),
-                     "kernel_us_from": "per-launch HIP events" if args.eager else
-                                       "HIP events around the replayed launches / K (includes kernel boundaries)",
+                     "kernel_us_from": KERNEL_US_FROM[args.launch],
                      "alg_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }
@@ -341,17 +299,28 @@ def main():
         dist.destroy_process_group()
 
 
-def timed_launches(step_fn, dev, K, eager):
-    """Replay K launches (hipGraph chunks unless eager) between barrier +
-    synchronize; returns (elapsed s, ms per launch from HIP events on the
-    launch stream)."""
+def timed_launches(step_fn, dev, K, launch):
+    """Time K launches between barrier + synchronize; returns (elapsed s, ms
+    per launch from HIP events on the launch stream).
+
+    launch = "stream": the K launches are issued back to back on the stream
+    (asynchronous; the host stays ahead of a ~10 us kernel, so the GPU runs
+    them back to back and the first kernel starts at once).  "graph": they
+    are captured into hipGraphs (chunks of 100) that are instantiated and
+    uploaded (hipGraphUpload) before timing, then replayed.  "events": stream
+    launches, each bracketed by its own pair of HIP events (per-kernel time;
+    the event packets sit between the kernels)."""
+    import ctypes
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     stream = torch.cuda.current_stream(dev)
     graphs = []
-    if not eager:
+    if launch == "graph":
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         chunk = max(1, min(100, K))
         for c0 in range(0, K, chunk):
             g = torch.cuda.CUDAGraph()
@@ -360,26 +329,47 @@ def timed_launches(step_fn, dev, K, eager):
                 for i in range(c0, min(K, c0 + chunk)):
                     step_fn(i, cs)
             graphs.append(g)
+            assert hip.hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()),
+                                      ctypes.c_void_p(stream.cuda_stream)) == 0
         torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    if launch == "events":
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    if eager:
-        for i in range(K):
-            step_fn(i, stream.cuda_stream)
-    else:
+    if launch == "graph":
         for g in graphs:
             g.replay()
+    elif launch == "events":
+        for i in range(K):
+            starts[i].record(stream)
+            step_fn(i, stream.cuda_stream)
+            ends[i].record(stream)
+    else:
+        for i in range(K):
+            step_fn(i, stream.cuda_stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    if launch == "events":
+        return t1 - t0, sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K
     return t1 - t0, ev0.elapsed_time(ev1) / K
+
+
+KERNEL_US_FROM = {
+    "stream": "HIP events around the K back-to-back launches / K (includes kernel boundaries)",
+    "graph": "HIP events around the replayed launches / K (includes kernel boundaries)",
+    "events": "per-launch HIP events",
+}
+LAUNCH_DESC = {"stream": "back-to-back stream launches", "graph": "hipGraph replay (uploaded)",
+               "events": "stream launches with per-launch events"}
 
 
 def bench_super(args, c, B, cpu, world, rank, dev):
@@ -409,7 +399,7 @@ def bench_super(args, c, B, cpu, world, rank, dev):
     torch.cuda.synchronize(dev)
     env.check()
     elapsed, step_ms = timed_launches(lambda i, st: env.step_raw(actions[Wm + i].data_ptr(), rp, dp, st),
-                                      dev, K, args.eager)
+                                      dev, K, args.launch)
     env.check()
     stats = torch.stack([env.reward.sum(), env.done.to(torch.float64).sum()])
     stats, elapsed = reduce_run(stats, elapsed, world)
@@ -434,7 +424,7 @@ def bench_super(args, c, B, cpu, world, rank, dev):
         "vs_baseline": None, "dtype": "f64+u64+f32",
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * world,
-                   "launch": "eager" if args.eager else "hipGraph replay", "parallelism": f"env-shard x{world}",
+                   "launch": LAUNCH_DESC[args.launch], "parallelism": f"env-shard x{world}",
                    "auto_reset": True, "maxsteps": args.maxsteps},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "achieved_from": achieved_from,
@@ -442,7 +432,7 @@ def bench_super(args, c, B, cpu, world, rank, dev):
                                           "changed region (whole layer when max(d) changes)",
                      "kernel": "mcs::sg_step_kernel + mcs::sg_erode_kernel (one step)",
                      "kernel_us": round(step_ms * 1e3, 3),
-                     "kernel_us_from": "HIP events around the launches / K (both kernels of a step)",
+                     "kernel_us_from": KERNEL_US_FROM[args.launch] + " (both kernels of a step)",
                      "full_refresh_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }

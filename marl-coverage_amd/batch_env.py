@@ -139,7 +139,7 @@ class BatchCoverageEnv:
 
         if isinstance(self.sensor, LidarSensor):
             self._upload_beams(self.sensor)
-            self.sensor._listeners.append(self._upload_beams)
+            self.sensor.add_listener(self._upload_beams)
 
         if grids is not None:
             host = np.stack([grid_to_int8(p) for p in padded])
@@ -179,6 +179,8 @@ class BatchCoverageEnv:
         return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
 
     def _upload_beams(self, sensor):
+        if not getattr(self, "_h", None):  # closed
+            return
         tab = np.ascontiguousarray(sensor.table(), dtype=np.float64)
         self._cfg.num_beams = tab.shape[0]
         _lib.check(self.lib.mc_set_beam_table(self._h, tab.ctypes.data, tab.shape[0]),
@@ -189,6 +191,8 @@ class BatchCoverageEnv:
 
     def close(self):
         if getattr(self, "_h", None):
+            if isinstance(getattr(self, "sensor", None), LidarSensor):
+                self.sensor.remove_listener(self._upload_beams)
             self.lib.mc_destroy(self._h)
             self._h = None
 

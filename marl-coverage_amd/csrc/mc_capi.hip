@@ -344,6 +344,10 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       return fail(MC_EINVAL, "dist_reward: %d extended rows exceed the transform's %d", s.Wp + 2 * c.pad,
                   mc::dist_max_rows());
     }
+    if (s.Lp + 2 * c.pad > 32767) {  // the witness column is a signed 16-bit half (mc_device.h)
+      mc_destroy(E);
+      return fail(MC_EINVAL, "dist_reward: %d extended columns exceed 32767", s.Lp + 2 * c.pad);
+    }
     const size_t need = mc::dist_lds_bytes(s, c.pad);
     int maxlds = 0;
     if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
@@ -411,6 +415,10 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   if (!E || !host_table) return fail(MC_EINVAL, "mc_set_beam_table: null argument");
   if (E->s.sensor != MC_SENSOR_LIDAR) return fail(MC_EINVAL, "beam table on a non-lidar env");
   if (num_beams < 1) return fail(MC_EINVAL, "beam table needs >= 1 beam");
+  // the per-env LDS budget mc_create checked holds 16 B per beam: a new beam
+  // count must fit it too, or the next launch would fail inside HIP
+  if (mc::env_lds_bytes(E->s.N, E->s.TW, num_beams, E->s.TW <= 4 ? 4 : 8) > 65536)
+    return fail(MC_EINVAL, "mc_set_beam_table: %d beams exceed the 64 KiB per-env LDS window", num_beams);
   const int cmax = E->s.Wp > E->s.Lp ? E->s.Wp : E->s.Lp;
   std::vector<mc::Beam> bt(num_beams);
   std::vector<uint64_t> bits((size_t)num_beams * cmax, 0);

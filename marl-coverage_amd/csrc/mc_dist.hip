@@ -312,16 +312,18 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // comes from around the robot, so it keeps M valid longest)
     if (cov && vmax >= 0) {
       const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
-      atomicMax(&s_key, ((unsigned long long)vmax << 40) | ((unsigned long long)far << 24) |
-                            ((unsigned long long)ubest << 12) | (unsigned long long)vbest);
+      // 16 bits per field: d, far, u, v are all < 65535 (mc_create bounds
+      // width + length + 4 pad), so wide grids keep an exact witness
+      atomicMax(&s_key, ((unsigned long long)vmax << 48) | ((unsigned long long)far << 32) |
+                            ((unsigned long long)ubest << 16) | (unsigned long long)vbest);
     }
     __syncthreads();
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
-    const int M = cov ? (int)(s_key >> 40) : -1;
+    const int M = cov ? (int)(s_key >> 48) : -1;
     const float Mf = (float)M;
     if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
-      const int wu = (int)((s_key >> 12) & 0xFFF), wv = (int)(s_key & 0xFFF);
+      const int wu = (int)((s_key >> 16) & 0xFFFF), wv = (int)(s_key & 0xFFFF);
       reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
     }
     if (post) {

@@ -92,32 +92,46 @@ class DecGridRL:
         self._pad = max(self._egoradius, self._mini_map_rad)
         self._device = torch.device(device)
         self._envs = {}          # padded shape -> (BatchCoverageEnv, [pool grid ids])
-        self._pool_index = {}    # id(grid) -> (shape, index)
+        self._pool_index = {}    # id(caller's grid object) -> (padded shape, pool index)
         self._env = None
         self.reset(False, None)
         self._obs_dim = self.get_egocentric_observations()[0].shape
         self._num_actions = 4
 
     # ---- device env per padded grid shape ----------------------------------
-    def _device_env(self, grid):
-        padded_shape = (grid.shape[0] + 2, grid.shape[1] + 2)
-        if padded_shape not in self._envs:
-            pool = [g for g in list(self._train_gridlis or []) + list(self._test_gridlis or [])
-                    if np.asarray(g).shape == grid.shape]
+    def _device_env(self, raw):
+        """The pool env of ``raw``'s padded shape and ``raw``'s index in it.
+        The pool is keyed on the caller's own grid objects (the train/test
+        list entries): lists of lists are accepted like the reference's
+        ``np.pad`` accepts them, and converting them per reset would make a
+        new object every time."""
+        shape = np.asarray(raw).shape
+        padded_shape = (shape[0] + 2, shape[1] + 2)
+        uniq = self._envs[padded_shape][1] if padded_shape in self._envs else None
+        if uniq is None:
             uniq, seen = [], set()
-            for g in pool:
-                if id(g) not in seen:
+            for g in list(self._train_gridlis or []) + list(self._test_gridlis or []):
+                if id(g) not in seen and np.asarray(g).shape == shape:
                     seen.add(id(g))
                     uniq.append(g)
-            if not any(g is grid for g in uniq):
-                uniq.append(grid)
-            env = BatchCoverageEnv(self._env_config, 1, grids=uniq, device=self._device,
-                                   auto_reset=False, sensor=self._sensor,
+        hit = self._pool_index.get(id(raw))
+        if (padded_shape not in self._envs or hit is None or hit[0] != padded_shape
+                or uniq[hit[1]] is not raw):
+            if not any(g is raw for g in uniq):
+                # a grid outside the train/test lists (e.g. a list entry the
+                # caller replaced): the pool of its shape grows by one
+                uniq = uniq + [raw]
+            if padded_shape in self._envs:
+                self._envs.pop(padded_shape)[0].close()
+                if self._env is not None and self._env._h is None:
+                    self._env = None
+            env = BatchCoverageEnv(self._env_config, 1, grids=[np.asarray(g) for g in uniq],
+                                   device=self._device, auto_reset=False, sensor=self._sensor,
                                    want_adjacency=True)
             self._envs[padded_shape] = (env, uniq)
-        env, uniq = self._envs[padded_shape]
-        idx = next(i for i, g in enumerate(uniq) if g is grid)
-        return env, idx
+            self._pool_index.update({id(g): (padded_shape, i) for i, g in enumerate(uniq)})
+            hit = self._pool_index[id(raw)]
+        return self._envs[padded_shape][0], hit[1]
 
     def _push_done_thresh(self, env):
         t = self._torch.tensor([float(self._dt)], dtype=self._torch.float64)
@@ -158,7 +172,7 @@ class DecGridRL:
                 taken[x][y] = True
                 xs[count], ys[count] = x, y
                 count += 1
-        env, idx = self._device_env(np.asarray(raw))
+        env, idx = self._device_env(raw)
         if self._env is not env:
             self._env = env
             self._push_done_thresh(env)

@@ -8,6 +8,8 @@ the device march starts from the same float64 bits as the reference.
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 
 
@@ -35,11 +37,24 @@ class Sensor:
     sensor_type = None
 
     def __init__(self):
-        self._listeners = []
+        self._listeners = []     # weakref.WeakMethod of each device env's uploader
+
+    def add_listener(self, bound_method):
+        """Weakly register ``bound_method(sensor)``: a shared sensor must not
+        keep the device envs built on it alive."""
+        self._listeners.append(weakref.WeakMethod(bound_method))
+
+    def remove_listener(self, bound_method):
+        self._listeners = [w for w in self._listeners if w() is not None and w() != bound_method]
 
     def _changed(self):
-        for fn in self._listeners:
-            fn(self)
+        live = []
+        for w in self._listeners:
+            fn = w()
+            if fn is not None:
+                live.append(w)
+                fn(self)
+        self._listeners = live
 
 
 class LidarSensor(Sensor):

@@ -1,0 +1,90 @@
+"""GPU tests of the host-side API edges: grid pools given as lists of lists,
+sensors shared between envs, beam tables that outgrow the LDS budget."""
+import gc
+import weakref
+
+import numpy as np
+import pytest
+
+from oracle.cpu_ref import DecGridRLRef
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+def cfg(**kw):
+    c = dict(numrobot=2, maxsteps=1000, collision_penalty=5, done_thresh=1, done_incr=0,
+             terminal_reward=30, dist_reward=0, train_maxsteps=1000, test_maxsteps=1000,
+             egoradius=2, mini_map_rad=0, comm_radius=0, allow_comm=0, map_sharing=0,
+             single_square_tool=0, dijkstra_input=0, sensor_type="lidar",
+             sensor_config={"num_lasers": 9, "range": 4})
+    c.update(kw)
+    return c
+
+
+def test_list_grids_many_resets_match_oracle(torch_cuda):
+    """The reference np.pads whatever the train list holds, so lists of lists
+    work there (dec_grid_rl.py:466-472): every reset on them must too, across
+    grid shapes and with a list entry replaced between episodes."""
+    import marlcov
+    rs = np.random.RandomState(7)
+    mk = lambda w, l: np.where(rs.rand(w, l) < 0.15, -1.0, 1.0).tolist()  # noqa: E731
+    train = [mk(12, 12), mk(12, 12), mk(10, 14)]
+    c = cfg()
+    np.random.seed(3)
+    env = marlcov.DecGridRL(train, c)
+    np.random.seed(3)
+    ref = DecGridRLRef(train, c)
+    for ep in range(8):
+        if ep == 5:
+            train[1] = mk(12, 12)  # a new object of an existing shape
+        seed = 100 + ep
+        np.random.seed(seed)
+        o, g = env.reset(False, None)
+        np.random.seed(seed)
+        ro, rg = ref.reset(False, None)
+        np.testing.assert_array_equal(g, rg)
+        np.testing.assert_array_equal(o, ro)
+        for t in range(6):
+            a = int(rs.randint(0, 16))
+            o, r, d = env.step(a)
+            ro, rr, rd = ref.step(a)
+            tag = f"ep {ep} t {t}"
+            assert float(r) == float(rr), tag
+            assert bool(d) == bool(rd), tag
+            np.testing.assert_array_equal(o, ro, err_msg=tag)
+
+
+def test_shared_sensor_does_not_keep_envs_alive(torch_cuda):
+    import marlcov
+    c = cfg()
+    from marlcov.sensors import make_sensor
+    sensor = make_sensor(c)
+    grid = np.ones((16, 16))
+    e1 = marlcov.BatchCoverageEnv(c, 2, grids=[grid], sensor=sensor)
+    e2 = marlcov.BatchCoverageEnv(c, 2, grids=[grid], sensor=sensor)
+    w1 = weakref.ref(e1)
+    del e1
+    gc.collect()
+    assert w1() is None, "the sensor kept a device env alive"
+    e2.close()
+    sensor.set_thetalist(np.linspace(0, 2 * np.pi, 11, endpoint=False))  # no listener left to fail
+    assert sensor._listeners == []
+
+
+def test_beam_table_over_lds_budget_is_rejected(torch_cuda):
+    """A beam count that no longer fits the per-env LDS window mc_create
+    checked is refused when the table is set, with a clear error."""
+    import marlcov
+    env = marlcov.BatchCoverageEnv(cfg(), 1, grids=[np.ones((20, 20))])
+    with pytest.raises(Exception, match="LDS"):  # 16 B per beam: 4500 beams > 64 KiB
+        env.sensor.set_thetalist(np.linspace(0, 2 * np.pi, 4500, endpoint=False))
+    env.reset()
+    env.check()

@@ -122,6 +122,10 @@ BATCH_CASES = {
                                    sensor_config={"num_lasers": 9, "range": 4}),
                           lambda rs: bern(rs, 20, 20, 0.1), 6, 40),
     "dist_c5_like_n16": (base_cfg(numrobot=16, dist_reward=1), lambda rs: bern(rs, 64, 64, 0.1), 2, 6),
+    # wide, short grids: the witness column passes 4096 (the transform's
+    # packed max key keeps 16 bits per field)
+    "dist_wide_short": (base_cfg(numrobot=2, dist_reward=1, sensor_config={"num_lasers": 9, "range": 4}),
+                        lambda rs: bern(rs, 30, 4200, 0.1), 4, 20),
     # long episodes: max(d) drops many times (the env kernel's witness test
     # sends those maps to the full transform, the rest keep M and take their
     # targets from the window search); single_square_tool keeps coverage thin

@@ -251,3 +251,30 @@ def test_episode_config_cut():
     c = dict(maxsteps=20, train_maxsteps=300, test_maxsteps=50)
     assert episode_config(c, testing=True)["maxsteps"] == 20
     assert c["maxsteps"] == 20  # the caller's dict is not modified
+
+
+def test_sensor_listeners_are_weak():
+    """A sensor shared by several device envs holds them weakly (a dropped
+    env is not kept alive and is skipped on set_thetalist)."""
+    import gc
+
+    from marlcov.sensors import LidarSensor
+    calls = []
+
+    class Holder:
+        def upload(self, sensor):
+            calls.append(sensor._num_lasers)
+
+    s = LidarSensor({"num_lasers": 5, "range": 3})
+    a, b = Holder(), Holder()
+    s.add_listener(a.upload)
+    s.add_listener(b.upload)
+    s.set_thetalist(np.linspace(0, 2 * np.pi, 7, endpoint=False))
+    assert calls == [7, 7]
+    del a
+    gc.collect()
+    s.set_thetalist(np.linspace(0, 2 * np.pi, 9, endpoint=False))
+    assert calls == [7, 7, 9] and len(s._listeners) == 1
+    s.remove_listener(b.upload)
+    s.set_thetalist(np.linspace(0, 2 * np.pi, 3, endpoint=False))
+    assert calls == [7, 7, 9] and s._listeners == []

@@ -1,0 +1,12 @@
+# Round-2 check: all GPU tests, then the bench in the driver's short form and
+# the default form (stream launches) and the graph form.
+set -u
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/r2check"; mkdir -p "$OUT"
+cd "$R"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+rc=$?; tail -3 "$OUT/gpu_tests.log"; [ $rc -ne 0 ] && exit $rc
+for args in "--steps 20 --warmup 5" "" "--launch graph --steps 20 --warmup 5" "--launch graph"; do
+  timeout -k 10 300 python3 bench.py --no-cpu $args > "$OUT/b.json" 2> "$OUT/b.err" || exit 1
+  python3 -c "import json; d=json.load(open('$OUT/b.json')); print('$args', d['value'], d['ms_per_step'], d['roofline']['kernel_us'])"
+done
+exit 0
