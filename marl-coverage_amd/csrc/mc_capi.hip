@@ -423,6 +423,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   std::vector<mc::Beam> bt(num_beams);
   std::vector<uint64_t> bits((size_t)num_beams * cmax, 0);
   int kmax = 0;
+  bool common = true;
   for (int b = 0; b < num_beams; ++b) {
     const double xi = host_table[3 * b], yi = host_table[3 * b + 1], di = host_table[3 * b + 2];
     mc::Beam& o = bt[b];
@@ -436,7 +437,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
       return fail(MC_EINVAL, "beam %d is not a normalised lidar.py increment (%g, %g)", b, xi, yi);
     }
     o.msign = minor > 0 ? 1 : (minor < 0 ? -1 : 0);
-    o.pad_ = 0;
+    o.bits = 0;
     if (!(di >= 1.0)) return fail(MC_EINVAL, "beam %d distinc %g < 1", b, di);
     // currdist = 0; while currdist < range: currdist += distinc  (lidar.py:49-56)
     double dist = 0.0;
@@ -466,6 +467,31 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
       }
       bits[(size_t)b * cmax + c0] = w;
     }
+    // the pattern of most starts; it stands for the beam's table when every
+    // start a robot can occupy (1 .. cm-2: the border is -1) visits the same
+    // cells with it up to the first border cell of the minor axis, where the
+    // march ends (an obstacle) -- then the rest of the word is never read
+    {
+      const uint64_t* row = &bits[(size_t)b * cmax];
+      uint64_t best = row[cm > 2 ? 1 : 0];
+      int best_n = 0;
+      for (int c0 = 1; c0 + 1 < cm; ++c0) {
+        int n = 0;
+        for (int c1 = 1; c1 + 1 < cm; ++c1) n += row[c1] == row[c0];
+        if (n > best_n) { best_n = n; best = row[c0]; }
+        if (2 * n > cm) break;
+      }
+      o.bits = (uint32_t)best;
+      for (int c0 = 1; c0 + 1 < cm && common; ++c0) {
+        int a = c0, c = c0;  // cell of the start's own word / of the common word
+        for (int k = 0; k < K; ++k) {
+          a += ((row[c0] >> k) & 1) ? o.msign : 0;
+          c += ((best >> k) & 1) ? o.msign : 0;
+          if (a != c) { common = false; break; }
+          if (a <= 0 || a >= cm - 1) break;  // border reached: the march ends here
+        }
+      }
+    }
   }
   HIP_TRY(hipSetDevice(E->device));
   if (num_beams != E->beam_count || !E->beams_buf) {
@@ -492,6 +518,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   HIP_TRY(hipMemcpy((void*)E->s.beam_bits, bits.data(), bits.size() * sizeof(uint64_t),
                     hipMemcpyHostToDevice));
   E->s.beam_kmax = kmax;
+  E->s.beam_common = common && !getenv("MARLCOV_BEAM_TABLE") ? 1 : 0;
   E->beams_set = true;
   return MC_OK;
 }

@@ -435,7 +435,9 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   R.d0 = (uint32_t)(ax ? bm.sign * RB : bm.sign);
   R.d1 = (uint32_t)(ax ? bm.msign : bm.msign * RB);
   R.K = R.live ? bm.K : -1;
-  R.bits = R.live ? (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)] : 0u;
+  R.bits = !R.live ? 0u
+           : s.beam_common ? bm.bits
+                           : (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)];
   return R;
 }
 

@@ -31,7 +31,7 @@ struct Beam {
   int16_t axis;   // 0: major axis is x (rows), 1: major axis is y (columns)
   int16_t sign;   // +1 / -1 along the major axis
   int32_t msign;  // +1 / -1 / 0: direction of a minor-axis move
-  int32_t pad_;
+  uint32_t bits;  // the step bits shared by every start (State::beam_common)
 };
 static_assert(sizeof(Beam) == 16, "Beam is 16 bytes");
 
@@ -72,6 +72,11 @@ struct State {
   const uint64_t* beam_bits;  // [nbeams][bcmax] minor-move bits per start coordinate
   int bcmax;                  // max(Wp, Lp)
   int beam_kmax;              // max Beam::K (<= H): march steps of a pass
+  // 1: every beam marches the same minor steps (Beam::bits) from every start
+  // coordinate a robot can occupy, up to the step where it reaches the
+  // grid's border (an obstacle, so the march ends there): the march needs no
+  // beam_bits load (mc_set_beam_table checks this on the host)
+  int beam_common;
   int32_t* env_grid;
   int32_t* pos;
   uint64_t* moved;

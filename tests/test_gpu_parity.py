@@ -410,3 +410,12 @@ def test_auto_reset_random_grid_pool(torch_cuda):
             compare_env(st, b, refs[b], f"t={t} env {b}")
     assert len(used) >= 4  # the draws cover the pool
     env.check()
+
+
+@pytest.mark.parametrize("name", ["c2_like_n4_128", "c4_like_n8_256_360beams", "nonsquare_70x150_r12"])
+def test_batch_matches_oracle_full_beam_table(torch_cuda, name, monkeypatch):
+    """The same cases with the per-start beam table forced on (the march
+    otherwise uses each beam's common step bits when the host proves them
+    equivalent: mc_set_beam_table, State::beam_common)."""
+    monkeypatch.setenv("MARLCOV_BEAM_TABLE", "1")
+    test_batch_matches_oracle(torch_cuda, name)
