@@ -128,8 +128,10 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
 template <int NT, int EPW, typename WT>
 struct Ctx {
   static constexpr int LPE = NT / EPW;            // lanes per env
-  static constexpr int KI = kMaxItemsPerLane;     // staged tiles per lane
-  static constexpr int RPL = EPW == 1 ? 2 : 3;    // beams per lane per pass (C4 A/B: 4 or 6 are slower)
+  static constexpr int KI = EPW >= 4 ? 2 * kMaxItemsPerLane : kMaxItemsPerLane;  // staged tiles per lane
+  // beams per lane per pass (C4 A/B: 4 or 6 are slower with one env per
+  // workgroup); four envs per wave march up to 6 x 16 rays in one pass
+  static constexpr int RPL = EPW == 1 ? 2 : (EPW == 2 ? 3 : 6);
   int sub;    // lane within the env
   int lane0;  // first lane of this env's slot within the wave
   int e;      // env index
@@ -160,6 +162,7 @@ struct Items {
   bool in[KI];          // tile inside the map (and item live)
   uint64_t f[KI], o[KI], u[KI];     // old free / obst / union tiles (raw loads)
   uint64_t nf[KI], no[KI], nu[KI];  // newly set bits
+  uint64_t mf[KI], mo[KI];          // lidar: this step's free / obstacle marks (gather_marks)
   bool masks;                       // f / o / u were loaded (else known zero)
 };
 
@@ -465,6 +468,8 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
 #if defined(MC_ABL) && MC_ABL == 1
   lds_or<WT>(sink, bit);  // timing ablation: no marks
 #else
+  // (two exec-masked ORs at fixed plane offsets instead of the address
+  // selects were slower: 10.52 vs 10.04 us at C2)
   WT* tgt = const_cast<WT*>(ray_word<WT>(hit ? L.opr : L.fpr, R));
   lds_or<WT>((on && !dup) ? tgt : sink, bit);
 #endif
@@ -556,22 +561,25 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
 }
 
 // lidar: mark rows -> mark tiles (after the march, before the merge)
-template <int NT, int EPW, typename WT>
-__device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
+// The lane keeps its items' marks in registers for the merge; only the free
+// marks go to LDS (other lanes' union dedup reads them).
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
-  constexpr int KI = Ctx<NT, EPW, WT>::KI;
   const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   const int items = s.N * TW2;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const int idx = C.sub + k * LPE;
+    I.mf[k] = I.mo[k] = 0;
     if (idx < items) {
       const int a = udiv(idx, s.mg_TW2), rem = idx - a * TW2;
       const int ti = udiv(rem, s.mg_TW), tj = rem - ti * TW;
       const int r0 = a * (8 * TW + 1) + 8 * ti;
-      L.fp[idx] = gather_tile<WT>(L.fpr, r0, tj);
-      L.op[idx] = gather_tile<WT>(L.opr, r0, tj);
+      I.mf[k] = gather_tile<WT>(L.fpr, r0, tj);
+      I.mo[k] = gather_tile<WT>(L.opr, r0, tj);
+      L.fp[idx] = I.mf[k];
     }
   }
 }
@@ -598,12 +606,23 @@ __device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW, W
 // every block that holds it.  Also folds the marks into the old tiles (the
 // obs crops read the post-step maps).
 // --------------------------------------------------------------------------
-template <int NT, int EPW, typename WT, int KI>
-__device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I) {
+template <int NT, int EPW, typename WT, int KI, int NS>
+__device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I,
+                                      bool marks_in_regs) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const Lds<WT>& L = C.L;
   const int TW = s.TW;
   const int items = s.N * TW * TW;
+  // compile-time agent count: every lower agent's block origin once, in
+  // registers (broadcast LDS reads issued together)
+  int BX[NS > 0 ? NS : 1], BY[NS > 0 ? NS : 1];
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int b = 0; b < NS; ++b) {
+      BX[b] = L.bx[b];
+      BY[b] = L.by[b];
+    }
+  }
   // EPW == 1: agent j's block origin in lane j of every wave, broadcast by
   // v_readlane (N <= 64)
   const int jw = (int)(threadIdx.x & 63);
@@ -615,7 +634,8 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
     const int idx = C.sub + k * LPE;
     I.nf[k] = I.no[k] = I.nu[k] = 0;
     if (idx < items) {
-      const uint64_t fp = L.fp[idx], op = L.op[idx];
+      const uint64_t fp = marks_in_regs ? I.mf[k] : L.fp[idx];
+      const uint64_t op = marks_in_regs ? I.mo[k] : L.op[idx];
       uint64_t f0, o0, u0;
       old_tiles<KI>(I, k, f0, o0, u0);  // first use of the mask loads
       I.f[k] = f0;
@@ -628,13 +648,25 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       uint64_t cand = fp & ~u0;
       const int a = I.a[k], gi = I.gi[k], gj = I.gj[k];
 #if defined(MC_ABL) && MC_ABL == 4
-      for (int b = 0; b < 0; ++b) {  // timing ablation: no dedup
+      if constexpr (false) {  // timing ablation: no dedup
 #else
-      // marks of lower-index agents in this tile (bounded by N-1 so a
-      // compile-time N unrolls it: the reads of all b are then in flight)
+      if constexpr (NS > 0) {
+#endif
+        // marks of lower-index agents in this tile: every read issued
+        // unconditionally (own tile when unused), no loop-carried branch
+        uint64_t t[NS > 1 ? NS - 1 : 1];
+        bool use[NS > 1 ? NS - 1 : 1];
+#pragma unroll
+        for (int b = 0; b < NS - 1; ++b) {
+          const int bi = gi - BX[b], bj = gj - BY[b];
+          use[b] = b < a && (unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW;
+          t[b] = L.fp[use[b] ? (b * TW + bi) * TW + bj : idx];
+        }
+#pragma unroll
+        for (int b = 0; b < NS - 1; ++b) cand &= use[b] ? ~t[b] : ~0ull;
+      } else {
       for (int b = 0; b < s.N - 1; ++b) {
         if (b >= a) break;
-#endif
         int bxb, byb;
         if constexpr (EPW == 1) {
           bxb = rdlane(abx, b);
@@ -646,6 +678,7 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
         const int bi = gi - bxb, bj = gj - byb;
         if ((unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW)
           cand &= ~L.fp[(b * TW + bi) * TW + bj];
+      }
       }
       I.nu[k] = cand;
       cv += __popcll(cand);
@@ -681,7 +714,7 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 }
 
 // sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
-template <int NT, int EPW, typename WT, int KI, int SUK>
+template <int NT, int EPW, typename WT, int KI, int SUK, int NS>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
 #if !(defined(MC_ABL) && MC_ABL == 3)
@@ -690,7 +723,7 @@ __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EP
   __syncthreads();
   STAMP(13);
   if (s.sensor == 0) {
-    gather_marks<NT, EPW, WT>(s, C);
+    gather_marks<NT, EPW, WT, KI>(s, C, I);
     __syncthreads();
   }
   STAMP(4);
@@ -698,7 +731,7 @@ __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EP
     single_tool<NT, EPW, WT>(s, C);
     __syncthreads();
   }
-  merge<NT, EPW, WT, KI>(s, C, I);
+  merge<NT, EPW, WT, KI, NS>(s, C, I, s.sensor == 0 && !s.sst);
 }
 
 // --------------------------------------------------------------------------
@@ -715,7 +748,7 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK>
+template <int NT, int EPW, typename WT, int SUK, int NS>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -792,7 +825,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
-  sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK, NS>(s, C, I);
   store_tiles<NT, EPW, WT, KI>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
@@ -902,6 +935,76 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>
   }
 }
 
+// Compile-time obs shape (3 layers, E*E <= 28 bits, whole dwords per env):
+// lane j < 3N of a slot builds the E*E-bit crop of block j = (agent j / 3,
+// layer j % 3) -- layer 0 from the robot cells, layers 1 and 2 from one LDS
+// byte per crop row and tile (the crop's bytes in the post-step tiles).  The
+// wave's envs are consecutive, so their obs are one run of dwords: lane l
+// writes dwords l, l + 64, ...; dword d is the nibble at bit 4d of the
+// slot's crop stream (fetched from the crop lanes by ds_bpermute), spread to
+// bytes by one multiply.  No per-row or per-layer branches.
+template <int EGO, int NS>
+struct ObsFast {
+  static constexpr int E = 2 * EGO + 1, EE = E * E, NB = 3 * NS;
+  static constexpr bool ok = EGO > 0 && NS > 0 && EE <= 28 && (NB * EE) % 4 == 0;
+};
+
+template <int NT, int EPW, typename WT, int NS, int EGO>
+__device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW, WT>& C,
+                                               uint8_t* obs_out) {
+  using OF = ObsFast<EGO, NS>;
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int E = OF::E, EE = OF::EE, NB = OF::NB;
+  static_assert(NB <= LPE, "one crop per lane");
+  const Lds<WT>& L = C.L;
+  const int TW = s.TW;
+  // ---- crops
+  const int j = C.sub < NB ? C.sub : 0;
+  const int a = (j * 86) >> 8;  // j / 3 for j < 128
+  const int layer = j - 3 * a;
+  const int xa = L.x[a], ya = L.y[a];
+  const uint64_t moved = L.sc->moved;
+  uint32_t rp = 0;  // layer 0: robot_pad crop (robots that moved since the reset)
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int dx = L.x[i] - xa + EGO, dy = L.y[i] - ya + EGO;
+    const bool on = ((moved >> i) & 1) && (unsigned)dx < (unsigned)E && (unsigned)dy < (unsigned)E;
+    rp |= on ? (1u << (dx * E + dy)) : 0u;
+  }
+  // layers 1, 2: crop row r = bits [ly0 & 7, +E) of bytes (lx & 7) of tiles
+  // (lx >> 3, ly0 >> 3) and the next tile column
+  const uint8_t* plane = reinterpret_cast<const uint8_t*>(layer == 2 ? L.oold : L.fold);
+  const int lx0 = xa - EGO - 8 * L.bx[a], ly0 = ya - EGO - 8 * L.by[a];
+  const uint8_t* t0 = plane + ((size_t)(a * TW) * TW + (ly0 >> 3)) * 8;
+  uint32_t fo = 0;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int lx = lx0 + r;
+    const uint8_t* p = t0 + (size_t)(lx >> 3) * TW * 8 + (lx & 7);
+    const uint32_t w = (uint32_t)p[0] | ((uint32_t)p[8] << 8);
+    fo |= ((w >> (ly0 & 7)) & ((1u << E) - 1u)) << (r * E);
+  }
+  const uint32_t crop = layer == 0 ? rp : fo;
+  // ---- dwords of the wave's obs run
+  constexpr int DPE = NB * EE / 4;       // dwords per env (a cell is one byte)
+  constexpr int D = EPW * DPE;           // dwords per wave
+  const int e_first = blockIdx.x * EPW;  // the wave's first env
+  uint32_t* out = reinterpret_cast<uint32_t*>(obs_out + (size_t)e_first * (NB * EE));
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    const int es = EPW == 1 ? 0 : d / DPE;  // env slot of dword d
+    const int i = 4 * (d - es * DPE);       // its first bit within that env's stream
+    const int jb = i / EE, o = i - jb * EE;
+    const int src = es * LPE + jb;
+    const uint32_t w0 = (uint32_t)__shfl((int)crop, src);
+    const uint32_t w1 = (uint32_t)__shfl((int)crop, src + 1 < 64 ? src + 1 : src);
+    const uint32_t nib = ((w0 | (w1 << EE)) >> o) & 0xFu;
+    if (d < D && e_first + es < s.B) out[d] = (nib * 0x00204081u) & 0x01010101u;
+  }
+}
+
 // --------------------------------------------------------------------------
 // the env kernel: EPW envs per workgroup
 // --------------------------------------------------------------------------
@@ -921,6 +1024,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // march steps per batch: the whole march when the shape fixes a short
   // beam_kmax, a quarter of a long one (register pressure)
   constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
+  constexpr int NSM = (SH::N > 0 && SH::N <= 8) ? SH::N : 0;  // compile-time agent count, if small
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1012,7 +1116,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
     __syncthreads();
     STAMP(3);
-    sense_and_merge<NT, EPW, WT, KI, SUK>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK, NSM>(s, C, I);
     __syncthreads();
     STAMP(5);
     if (C.sub == 0) {
@@ -1059,7 +1163,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       store_tiles<NT, EPW, WT, KI>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
@@ -1068,7 +1172,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM>(s, C, reset_req ? inj_pos : nullptr);
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
     // obs of the current state only (dec_grid_rl.py:104-107,160)
@@ -1096,7 +1200,15 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   }
   STAMP(8);
 #if !(defined(MC_ABL) && MC_ABL == 5)
-  if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
+#ifdef MC_OBS_SLOW
+  if constexpr (false) {
+#else
+  if constexpr (ObsFast<SH::EGO, SH::N>::ok && NT == 64 && ObsFast<SH::EGO, SH::N>::NB <= CtxT::LPE) {
+#endif
+    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO>(s, C, obs_out);  // every lane of the wave
+  } else {
+    if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
+  }
 #endif
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
@@ -1119,6 +1231,14 @@ int env_pack(const State& s) {
   const int items = s.N * s.TW * s.TW;
   const int rays = s.sensor == 0 ? s.N * s.nbeams : 0;
   return (s.N <= 32 && items <= kMaxItemsPerLane * 32 && rays <= 3 * 32) ? 2 : 1;
+}
+
+// Whether an env also fits 16 lanes (four envs per wave: N <= 16, at most
+// 2 * KI staged tiles and 6 beams per lane).
+bool env_fits_quarter(const State& s) {
+  const int items = s.N * s.TW * s.TW;
+  const int rays = s.sensor == 0 ? s.N * s.nbeams : 0;
+  return s.N <= 16 && items <= 2 * kMaxItemsPerLane * 16 && rays <= 6 * 16;
 }
 
 // MARLCOV_SPECIALIZE=0 forces the generic (runtime-shape) kernels (A/B tests)
@@ -1144,7 +1264,11 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
   using Dynamic = Shape<0, 0, 0, 0, 0>;
   using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
   using ShapeC4 = Shape<8, 20, 360, 2, 20>; // 360 beams, R=20
-  if (epw == 2) {
+  if (epw == 4) {
+    if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 4, uint32_t, ShapeC2);
+    else if (narrow) MC_LAUNCH(64, 4, uint32_t);
+    else MC_LAUNCH(64, 4, uint64_t);
+  } else if (epw == 2) {
     if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
