@@ -20,7 +20,6 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
                       uint8_t* adj, int nt, int epw, hipStream_t stream);
 int env_pack(const State& s);
-bool env_fits_quarter(const State& s);
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream);
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
@@ -142,9 +141,7 @@ int launch_epw(const Env* E) {
     const char* v = getenv("MARLCOV_EPW");
     return v ? atoi(v) : 0;
   }();
-  if (force == 1) return 1;
-  if (force == 4 && E->epw == 2 && mc::env_fits_quarter(E->s)) return 4;
-  return E->epw;
+  return force == 1 ? 1 : E->epw;
 }
 
 }  // namespace

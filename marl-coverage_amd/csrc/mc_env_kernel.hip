@@ -128,10 +128,8 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
 template <int NT, int EPW, typename WT>
 struct Ctx {
   static constexpr int LPE = NT / EPW;            // lanes per env
-  static constexpr int KI = EPW >= 4 ? 2 * kMaxItemsPerLane : kMaxItemsPerLane;  // staged tiles per lane
-  // beams per lane per pass (C4 A/B: 4 or 6 are slower with one env per
-  // workgroup); four envs per wave march up to 6 x 16 rays in one pass
-  static constexpr int RPL = EPW == 1 ? 2 : (EPW == 2 ? 3 : 6);
+  static constexpr int KI = kMaxItemsPerLane;     // staged tiles per lane
+  static constexpr int RPL = EPW == 1 ? 2 : 3;    // beams per lane per pass (C4 A/B: 4 or 6 are slower)
   int sub;    // lane within the env
   int lane0;  // first lane of this env's slot within the wave
   int e;      // env index
@@ -1112,11 +1110,23 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     const int numfree = s.numfree[g0];
     __syncthreads();
     STAMP(2);
+#if defined(MC_ABL) && MC_ABL == 10
+    // timing ablation: the memory floor (no moves, sensing, merge or obs)
+#pragma unroll
+    for (int k = 0; k < KI; ++k) I.nf[k] = I.no[k] = I.nu[k] = 0;
+#else
+#if defined(MC_ABL) && MC_ABL == 7
+    // timing ablation: no moves
+#else
+    // (the same loop on the scalar unit, robots read by v_readlane, was
+    // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
     if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
     else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
+#endif
     __syncthreads();
     STAMP(3);
     sense_and_merge<NT, EPW, WT, KI, SUK, NSM>(s, C, I);
+#endif
     __syncthreads();
     STAMP(5);
     if (C.sub == 0) {
@@ -1199,7 +1209,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
   }
   STAMP(8);
-#if !(defined(MC_ABL) && MC_ABL == 5)
+#if !(defined(MC_ABL) && (MC_ABL == 5 || MC_ABL == 10))
 #ifdef MC_OBS_SLOW
   if constexpr (false) {
 #else
@@ -1233,13 +1243,6 @@ int env_pack(const State& s) {
   return (s.N <= 32 && items <= kMaxItemsPerLane * 32 && rays <= 3 * 32) ? 2 : 1;
 }
 
-// Whether an env also fits 16 lanes (four envs per wave: N <= 16, at most
-// 2 * KI staged tiles and 6 beams per lane).
-bool env_fits_quarter(const State& s) {
-  const int items = s.N * s.TW * s.TW;
-  const int rays = s.sensor == 0 ? s.N * s.nbeams : 0;
-  return s.N <= 16 && items <= 2 * kMaxItemsPerLane * 16 && rays <= 6 * 16;
-}
 
 // MARLCOV_SPECIALIZE=0 forces the generic (runtime-shape) kernels (A/B tests)
 static bool getenv_spec() {
@@ -1264,11 +1267,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
   using Dynamic = Shape<0, 0, 0, 0, 0>;
   using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
   using ShapeC4 = Shape<8, 20, 360, 2, 20>; // 360 beams, R=20
-  if (epw == 4) {
-    if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 4, uint32_t, ShapeC2);
-    else if (narrow) MC_LAUNCH(64, 4, uint32_t);
-    else MC_LAUNCH(64, 4, uint64_t);
-  } else if (epw == 2) {
+  if (epw == 2) {
     if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
