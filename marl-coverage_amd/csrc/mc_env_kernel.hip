@@ -481,7 +481,7 @@ __device__ __forceinline__ const WT* ray_word(const WT* plane, const Ray& R) {
 // cells: fewer same-address LDS atomics).  Returns whether the ray marked.
 template <typename WT>
 __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow, WT* sink,
-                                         bool dup) {
+                                         bool dup, bool frow_valid) {
   const bool on = R.live && k <= R.K;
   const WT bit = (WT)1 << (R.P & (8 * sizeof(WT) - 1));
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
@@ -492,7 +492,11 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
   // (two exec-masked ORs at fixed plane offsets instead of the address
   // selects were slower: 10.52 vs 10.04 us at C2)
   WT* tgt = const_cast<WT*>(ray_word<WT>(hit ? L.opr : L.fpr, R));
-  lds_or<WT>((on && !dup) ? tgt : sink, bit);
+  if (frow_valid) {  // dense: most rays skip; an exec-masked OR of the few that mark
+    if (on && !dup) lds_or<WT>(tgt, bit);
+  } else {
+    lds_or<WT>((on && !dup) ? tgt : sink, bit);
+  }
 #endif
   R.live = on && !hit;
   return on;
@@ -556,7 +560,7 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
             for (int j = 0; j < RPL; ++j) {
               const bool dup = dense && prev_on && q[j].P == prev_p;
               prev_p = q[j].P;
-              prev_on = ray_mark<WT>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink, dup);
+              prev_on = ray_mark<WT>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink, dup, dense);
               ray_advance(q[j], k0 + u);
             }
           }
