@@ -75,12 +75,15 @@ static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 // One env slot's LDS.  Tile planes are [N][TW][TW] u64 in the agent's block
 // coordinates.  Row planes are [N][8*TW+1] WT: row lx of agent a's block, bit ly
 // = cell (8*bx + lx, 8*by + ly); the lidar march and the moves read them.
-// negr: grid < 0; fldr: the agent's old free map (dense beam sets: cells a
-// ray need not mark again); fpr / opr: this step's free / obstacle marks.
+// negr: grid < 0; fldr: the cells the agent has seen (dense beam sets: cells
+// a ray need not mark again); fpr: every cell a ray visited this step -- its
+// free marks are the cells with grid >= 0, its obstacle marks the others
+// (a ray marks free cells up to the first obstacle, and that obstacle), so
+// one plane and one target per mark, split by the grid tile in the merge.
 template <typename WT>
 struct Lds {
   uint64_t *neg, *pos, *fold, *oold, *fp, *op;
-  WT *negr, *fldr, *fpr, *opr;
+  WT *negr, *fldr, *fpr;
   Beam* beams;
   int32_t *x0, *y0, *x, *y;  // pre-move / post-move cells
   int32_t *bx, *by;          // tile-block origin (tile units) of each agent
@@ -105,9 +108,8 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   char* q = smem + (size_t)6 * tiles * 8;
   L.negr = reinterpret_cast<WT*>(q);
   L.fpr = L.negr + rows;
-  L.opr = L.fpr + rows;
-  L.fldr = L.opr + rows;
-  q += (((size_t)4 * rows * sizeof(WT)) + 15) & ~(size_t)15;
+  L.fldr = L.fpr + rows;
+  q += (((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15;
   L.beams = reinterpret_cast<Beam*>(q);
   q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
   L.x0 = reinterpret_cast<int32_t*>(q);
@@ -164,6 +166,7 @@ struct Items {
   uint64_t f[KI], o[KI], u[KI];     // old free / obst / union tiles (raw loads)
   uint64_t nf[KI], no[KI], nu[KI];  // newly set bits
   uint64_t mf[KI], mo[KI];          // lidar: this step's free / obstacle marks (gather_marks)
+  uint64_t n[KI];                   // grid < 0 tiles (outside the map: all ones)
   bool masks;                       // f / o / u were loaded (else known zero)
 };
 
@@ -258,6 +261,7 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     const int idx = C.sub + k * LPE;
     if (idx < items) {
       const uint64_t nt = in ? n[k] : ~0ull;  // outside the map: blocked (isInBounds)
+      I.n[k] = nt;
       if (square) {
         L.neg[idx] = nt;
         L.pos[idx] = in ? p[k] : 0ull;
@@ -311,7 +315,6 @@ __device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT
   if (s.sensor != 0) return;
   for (int r = C.sub; r < s.N * (8 * s.TW + 1); r += LPE) {
     C.L.fpr[r] = 0;
-    C.L.opr[r] = 0;
   }
 }
 
@@ -491,7 +494,7 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
 #else
   // (two exec-masked ORs at fixed plane offsets instead of the address
   // selects were slower: 10.52 vs 10.04 us at C2)
-  WT* tgt = const_cast<WT*>(ray_word<WT>(hit ? L.opr : L.fpr, R));
+  WT* tgt = const_cast<WT*>(ray_word<WT>(L.fpr, R));  // free or obstacle: the grid tells
   if (frow_valid) {  // dense: most rays skip; an exec-masked OR of the few that mark
     if (on && !dup) lds_or<WT>(tgt, bit);
   } else {
@@ -603,8 +606,9 @@ __device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, 
       const int a = udiv(idx, s.mg_TW2), rem = idx - a * TW2;
       const int ti = udiv(rem, s.mg_TW), tj = rem - ti * TW;
       const int r0 = a * (8 * TW + 1) + 8 * ti;
-      I.mf[k] = gather_tile<WT>(L.fpr, r0, tj);
-      I.mo[k] = gather_tile<WT>(L.opr, r0, tj);
+      const uint64_t m = gather_tile<WT>(L.fpr, r0, tj);
+      I.mf[k] = m & ~I.n[k];
+      I.mo[k] = m & I.n[k];
       L.fp[idx] = I.mf[k];
     }
   }

@@ -133,7 +133,7 @@ __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
 // rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
 __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes) {
   size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
-  b += (((size_t)4 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / fp / op / old free rows
+  b += (((size_t)3 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
   b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
   b += 64;                                             // scalars
