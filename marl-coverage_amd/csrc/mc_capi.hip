@@ -422,7 +422,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   const int cmax = E->s.Wp > E->s.Lp ? E->s.Wp : E->s.Lp;
   std::vector<mc::Beam> bt(num_beams);
   std::vector<uint64_t> bits((size_t)num_beams * cmax, 0);
-  int kmax = 0;
+  int kmax = 0, kmin = 1 << 30;
   bool common = true;
   for (int b = 0; b < num_beams; ++b) {
     const double xi = host_table[3 * b], yi = host_table[3 * b + 1], di = host_table[3 * b + 2];
@@ -447,6 +447,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
       return fail(MC_EINVAL, "beam %d takes %d steps > window half-width %d", b, K, E->s.H);
     o.K = K;
     kmax = K > kmax ? K : kmax;
+    kmin = K < kmin ? K : kmin;
     // the reference's minor-coordinate chain (currx/curry += inc, int() of it)
     // from every integer start; valid starts are the padded-grid interior
     const int cm = o.axis == 0 ? E->s.Lp : E->s.Wp;
@@ -518,6 +519,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   HIP_TRY(hipMemcpy((void*)E->s.beam_bits, bits.data(), bits.size() * sizeof(uint64_t),
                     hipMemcpyHostToDevice));
   E->s.beam_kmax = kmax;
+  E->s.beam_kmin = kmin;
   E->s.beam_common = common && !getenv("MARLCOV_BEAM_TABLE") ? 1 : 0;
   E->beams_set = true;
   return MC_OK;

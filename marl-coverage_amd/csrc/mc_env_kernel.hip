@@ -433,7 +433,9 @@ __device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT
 // (mc_set_beam_table rejects K > H).  Row planes: the cell's word is one add,
 // its bit one shift.
 // --------------------------------------------------------------------------
-// A ray's cell is packed as P = (row-plane byte offset << 6) | column: one
+typedef __attribute__((address_space(3))) char lds_char;
+
+// A ray's cell is packed as P = (row word's LDS address << 6) | column: one
 // add advances it, P >> 6 addresses the row word, and the shift amount of
 // 1 << P is taken mod the word width by the hardware.
 struct Ray {
@@ -455,7 +457,10 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   const int row = a * (8 * s.TW + 1) + xa - 8 * L.bx[a];
   const int col = ya - 8 * L.by[a];
   constexpr int RB = (int)sizeof(WT) * 64;  // one row in P units
-  R.P = ((uint32_t)row * RB) | (uint32_t)col;
+  // the row word's LDS address: P >> 6 is the neg-plane word's address
+  // itself (no per-step base add)
+  const uint32_t plane = (uint32_t)(uintptr_t)(const lds_char*)(const char*)L.negr;
+  R.P = ((plane + (uint32_t)row * (uint32_t)sizeof(WT)) << 6) | (uint32_t)col;
   const bool ax = bm.axis == 0;
   R.d0 = (uint32_t)(ax ? bm.sign * RB : bm.sign);
   R.d1 = (uint32_t)(ax ? bm.msign : bm.msign * RB);
@@ -471,9 +476,12 @@ __device__ __forceinline__ void ray_advance(Ray& R, int k) {
   R.P += R.d0 + (m & R.d1);
 }
 
+// the word of plane `plane` (a row plane of L, the same shape as negr) in
+// the ray's current row
 template <typename WT>
-__device__ __forceinline__ const WT* ray_word(const WT* plane, const Ray& R) {
-  return reinterpret_cast<const WT*>(reinterpret_cast<const char*>(plane) + (R.P >> 6));
+__device__ __forceinline__ const WT* ray_word(const Lds<WT>& L, const WT* plane, const Ray& R) {
+  const lds_char* p = (const lds_char*)(uintptr_t)(R.P >> 6) + (plane - L.negr) * (int)sizeof(WT);
+  return reinterpret_cast<const WT*>((const char*)p);
 }
 
 // Branch-free mark: every lane issues one ds_or per ray and step; a lane with
@@ -482,30 +490,36 @@ __device__ __forceinline__ const WT* ray_word(const WT* plane, const Ray& R) {
 // `dup`: the lane's previous ray (the adjacent beam) marks the same cell at
 // this step, so this one skips its atomic (near the robot adjacent beams share
 // cells: fewer same-address LDS atomics).  Returns whether the ray marked.
-template <typename WT>
-__device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow, WT* sink,
-                                         bool dup, bool frow_valid) {
-  const bool on = R.live && k <= R.K;
+template <typename WT, int KN>
+__device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow,
+                                         uint32_t sink_m, bool dup, bool frow_valid) {
+  // KN: a compile-time lower bound of every beam's K (steps k <= KN need no
+  // range test)
+  const bool on = R.live && (k <= KN || k <= R.K);
   const WT bit = (WT)1 << (R.P & (8 * sizeof(WT) - 1));
   const bool hit = (nrow & bit) != 0;  // oc[int(cx), int(cy)] < 0: the beam ends here
   dup |= (frow & bit) != 0;  // a cell the agent has seen: its mark is known (frow: 0 unless dense)
+  // mark-plane word = row word + a constant; a lane with nothing to mark
+  // selects its sink word less that constant (sink_m), so the constant rides
+  // in the instruction's offset field.  (Two exec-masked ORs at fixed plane
+  // offsets instead of the select were slower: 10.52 vs 10.04 us at C2.)
+  const int delta = (int)(L.fpr - L.negr) * (int)sizeof(WT);
 #if defined(MC_ABL) && MC_ABL == 1
-  lds_or<WT>(sink, bit);  // timing ablation: no marks
+  const uint32_t a = sink_m;  // timing ablation: no marks
 #else
-  // (two exec-masked ORs at fixed plane offsets instead of the address
-  // selects were slower: 10.52 vs 10.04 us at C2)
-  WT* tgt = const_cast<WT*>(ray_word<WT>(L.fpr, R));  // free or obstacle: the grid tells
+  const uint32_t a = (on && !dup) ? (R.P >> 6) : sink_m;
+#endif
+  WT* tgt = reinterpret_cast<WT*>((char*)((lds_char*)(uintptr_t)a + delta));  // free or obstacle: the grid tells
   if (frow_valid) {  // dense: most rays skip; an exec-masked OR of the few that mark
     if (on && !dup) lds_or<WT>(tgt, bit);
   } else {
-    lds_or<WT>((on && !dup) ? tgt : sink, bit);
+    lds_or<WT>(tgt, bit);
   }
-#endif
   R.live = on && !hit;
   return on;
 }
 
-template <int NT, int EPW, typename WT, int SUK>
+template <int NT, int EPW, typename WT, int SUK, int KN>
 __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   constexpr int RPL = Ctx<NT, EPW, WT>::RPL;
@@ -517,6 +531,8 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
     for (int a = C.sub; a < N; a += LPE)
       lds_or<WT>(&L.fpr[a * (8 * TW + 1) + L.x[a] - 8 * L.bx[a]], (WT)1 << (L.y[a] - 8 * L.by[a]));
     WT* sink = L.sink + (threadIdx.x & 63);
+    const uint32_t sink_m = (uint32_t)(uintptr_t)(const lds_char*)(const char*)sink -
+                            (uint32_t)((L.fpr - L.negr) * (int)sizeof(WT));
     const int total = N * s.nbeams;
     // lane l of a pass takes rays RPL*l .. RPL*l+RPL-1: within one ds_or the
     // lanes of an agent hold beams RPL apart, which mostly land in different
@@ -546,8 +562,8 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
           if (k0 + u <= kmax) {  // uniform
 #pragma unroll
             for (int j = 0; j < RPL; ++j) {
-              nr[u][j] = *ray_word<WT>(L.negr, q[j]);
-              fr[u][j] = dense ? *ray_word<WT>(L.fldr, q[j]) : (WT)0;
+              nr[u][j] = *ray_word<WT>(L, L.negr, q[j]);
+              fr[u][j] = dense ? *ray_word<WT>(L, L.fldr, q[j]) : (WT)0;
               ray_advance(q[j], k0 + u);
             }
           }
@@ -563,7 +579,7 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
             for (int j = 0; j < RPL; ++j) {
               const bool dup = dense && prev_on && q[j].P == prev_p;
               prev_p = q[j].P;
-              prev_on = ray_mark<WT>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink, dup, dense);
+              prev_on = ray_mark<WT, KN>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink_m, dup, dense);
               ray_advance(q[j], k0 + u);
             }
           }
@@ -744,11 +760,11 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 }
 
 // sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
-template <int NT, int EPW, typename WT, int KI, int SUK, int NS>
+template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
 #if !(defined(MC_ABL) && MC_ABL == 3)
-  sense<NT, EPW, WT, SUK>(s, C);
+  sense<NT, EPW, WT, SUK, KN>(s, C);
 #endif
   __syncthreads();
   STAMP(13);
@@ -778,7 +794,7 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int NS>
+template <int NT, int EPW, typename WT, int SUK, int NS, int KN>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -855,7 +871,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
-  sense_and_merge<NT, EPW, WT, KI, SUK, NS>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN>(s, C, I);
   store_tiles<NT, EPW, WT, KI>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
@@ -1157,7 +1173,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #endif
     __syncthreads();
     STAMP(3);
-    sense_and_merge<NT, EPW, WT, KI, SUK, NSM>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN>(s, C, I);
 #endif
     __syncthreads();
     STAMP(5);
@@ -1205,7 +1221,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       store_tiles<NT, EPW, WT, KI>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK, NSM>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM, SH::KN>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
@@ -1214,7 +1230,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK, NSM>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM, SH::KN>(s, C, reset_req ? inj_pos : nullptr);
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
     // obs of the current state only (dec_grid_rl.py:104-107,160)
@@ -1297,8 +1313,8 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
                      obs, adj)
 #define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
   using Dynamic = Shape<0, 0, 0, 0, 0>;
-  using ShapeC2 = Shape<4, 10, 21, 2, 10>;  // the bench workload
-  using ShapeC4 = Shape<8, 20, 360, 2, 20>; // 360 beams, R=20
+  using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;    // the bench workload
+  using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;  // 360 beams, R=20
   if (epw == 2) {
     if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);

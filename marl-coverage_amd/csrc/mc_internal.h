@@ -72,6 +72,7 @@ struct State {
   const uint64_t* beam_bits;  // [nbeams][bcmax] minor-move bits per start coordinate
   int bcmax;                  // max(Wp, Lp)
   int beam_kmax;              // max Beam::K (<= H): march steps of a pass
+  int beam_kmin;              // min Beam::K: steps k <= beam_kmin are in range for every beam
   // 1: every beam marches the same minor steps (Beam::bits) from every start
   // coordinate a robot can occupy, up to the step where it reaches the
   // grid's border (an obstacle, so the march ends there): the march needs no
@@ -152,14 +153,15 @@ __host__ __device__ inline size_t slot_stride(size_t slot_lds) {
 // (loop bounds, divisions and LDS offsets fold to constants and the march
 // unrolls); 0 leaves the field to the runtime State.  The launcher picks a
 // specialised instantiation only when the runtime State matches it exactly.
-template <int N_, int H_, int NB_, int EGO_, int KM_>
+template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0>
 struct Shape {
-  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_;
+  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
            (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
            (EGO_ == 0 || (s.ego == EGO_ && s.Lc == 3)) &&
-           (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_));
+           (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_)) &&
+           (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_));
   }
 };
 
@@ -186,6 +188,7 @@ __device__ __forceinline__ void specialize(State& s) {
     s.mg_LcE = magic_div(3 * (2 * SH::EGO + 1));
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
+  if constexpr (SH::KN > 0) s.beam_kmin = SH::KN;
   if constexpr (SH::EGO > 0) s.dist = 0;  // EGO matches only Lc == 3: no dist layer
 }
 
