@@ -1148,7 +1148,11 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   if (active) {
     STAMP(1);
     Items<KI> I;
-#if defined(MC_ABL) && MC_ABL == 6
+#if defined(MC_ABL) && MC_ABL == 12
+    // timing ablation: no second round trip (positions and scalars only)
+#pragma unroll
+    for (int k = 0; k < KI; ++k) { I.in[k] = false; I.a[k] = I.gi[k] = I.gj[k] = 0; }
+#elif defined(MC_ABL) && MC_ABL == 6
     stage<NT, EPW, WT, KI>(s, C, g0, false, I);  // timing ablation: grid tiles only
 #else
     stage<NT, EPW, WT, KI>(s, C, g0, true, I);  // ---- round trip 2 ----
@@ -1158,7 +1162,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     const int numfree = s.numfree[g0];
     __syncthreads();
     STAMP(2);
-#if defined(MC_ABL) && MC_ABL == 10
+#if defined(MC_ABL) && (MC_ABL == 10 || MC_ABL == 12)
     // timing ablation: the memory floor (no moves, sensing, merge or obs)
 #pragma unroll
     for (int k = 0; k < KI; ++k) I.nf[k] = I.no[k] = I.nu[k] = 0;
@@ -1257,7 +1261,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
   }
   STAMP(8);
-#if !(defined(MC_ABL) && (MC_ABL == 5 || MC_ABL == 10))
+#if !(defined(MC_ABL) && (MC_ABL == 5 || MC_ABL == 10 || MC_ABL == 12))
 #ifdef MC_OBS_SLOW
   if constexpr (false) {
 #else
