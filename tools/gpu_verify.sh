@@ -1,7 +1,7 @@
 # Round verification on one MI355X: every GPU test, smoke(), the default bench
 # line and the rocprofv3 kernel-trace summary of that same command.
 set -u
-R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/verify"; mkdir -p "$OUT"
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${VERIFY_TAG:-verify}"; mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 rc=$?; tail -3 "$OUT/gpu_tests.log"; [ $rc -ne 0 ] && exit $rc

@@ -62,7 +62,7 @@ def main():
         "config": args.config,
         "kernel": kname,
         "source": f"{args.dst}/pmc_*.csv (rocprofv3 --pmc, separate passes, "
-                  "bench.py --no-cpu --eager --steps 50)",
+                  "tools/gpu_pmc_traffic.sh)",
         "fetch_size_kb_per_launch": fetch,
         "write_size_kb_per_launch": write,
         "correction": "MI355X_MICROARCH.md HBM section: FETCH_SIZE reads 1/2 of the bytes of "
