@@ -187,28 +187,36 @@ __device__ __forceinline__ void lds_or(WT* p, WT v) {
 // less than the extra reads cost (measured: 10.9 vs 10.0 us at C2).
 __device__ __forceinline__ bool dense_beams(const State& s) { return s.sensor == 0 && s.nbeams >= 64; }
 
+// tile idx of a map array.  O32: the launcher checked that every byte offset
+// of the arrays fits 32 bits, so the address is the array base (uniform,
+// SGPRs) plus a 32-bit offset (one VGPR: global_load's saddr form, no
+// 64-bit address arithmetic per load)
+template <bool O32>
+__device__ __forceinline__ uint64_t ld_tile(const uint64_t* base, uint32_t idx) {
+  if constexpr (O32) return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(base) + (size_t)(idx << 3));
+  else return base[idx];
+}
+
 // --------------------------------------------------------------------------
 // stage: one round trip for every staged tile (masks known zero after reset)
 // --------------------------------------------------------------------------
-template <int NT, int EPW, typename WT, int KI>
+template <int NT, int EPW, typename WT, int KI, bool O32 = false>
 __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, int g,
                                       bool load_masks, Items<KI>& I) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
   const int items = s.N * TW2;
-  const size_t mt = (size_t)s.MT;
-  const uint64_t* gn = s.grid_neg + (size_t)g * mt;
-  const uint64_t* gp = s.grid_pos + (size_t)g * mt;
+  const uint32_t mt = (uint32_t)s.MT;
+  const uint32_t gb = __umul24((uint32_t)g, mt);  // this env's grid in the pool (tiles)
   const bool square = s.sensor == 1;
   uint64_t n[KI], p[KI];
   // 32-bit word indices (mc_create bounds every map array below 2^32 words);
   // products of 24-bit factors are single v_mul_u32_u24
   uint32_t gt[KI], fw[KI];
-  int ti[KI], tj[KI];
+  int ti[KI], tj[KI], bxa[KI], bya[KI];
   const uint32_t eN = (uint32_t)C.e * (uint32_t)s.N;
-  // addresses first, then every load of the lane back to back with no
-  // exec-mask branches (tiles outside the map read tile 0 and are replaced)
+  // every item's block origin read first (one LDS round trip for all items)
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const int idx = C.sub + k * LPE;
@@ -217,30 +225,38 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     const int rem = idx - a * TW2;
     ti[k] = udiv(rem, s.mg_TW);
     tj[k] = rem - ti[k] * TW;
-    const int gi = L.bx[a] + ti[k], gj = L.by[a] + tj[k];
     I.a[k] = a;
+    bxa[k] = L.bx[a];
+    bya[k] = L.by[a];
+  }
+  // addresses, then every load of the lane back to back with no exec-mask
+  // branches (tiles outside the map read tile 0 and are replaced)
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int idx = C.sub + k * LPE;
+    const int gi = bxa[k] + ti[k], gj = bya[k] + tj[k];
     I.gi[k] = gi;
     I.gj[k] = gj;
-    I.in[k] = it & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
-    gt[k] = I.in[k] ? tile_index(s.TCS, gi, gj) : 0u;
-    fw[k] = __umul24(eN + (uint32_t)a, (uint32_t)mt) + gt[k];
+    I.in[k] = (idx < items) & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
+    gt[k] = tile_index(s.TCS, I.in[k] ? gi : 0, I.in[k] ? gj : 0);
+    fw[k] = __umul24(eN + (uint32_t)I.a[k], mt) + gt[k];
   }
-  const uint32_t vw = __umul24((uint32_t)C.e, (uint32_t)mt);
+  const uint32_t vw = __umul24((uint32_t)C.e, mt);
   // grid tiles first: the moves and the march need only them, so the mask
   // tiles (needed from the merge on) stay in flight meanwhile (loads return
   // in order; the compiler waits only for what each use needs)
 #pragma unroll
-  for (int k = 0; k < KI; ++k) n[k] = gn[gt[k]];
+  for (int k = 0; k < KI; ++k) n[k] = ld_tile<O32>(s.grid_neg, gb + gt[k]);
   if (square) {
 #pragma unroll
-    for (int k = 0; k < KI; ++k) p[k] = gp[gt[k]];
+    for (int k = 0; k < KI; ++k) p[k] = ld_tile<O32>(s.grid_pos, gb + gt[k]);
   }
   if (load_masks) {
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
-      I.f[k] = s.freem[fw[k]];
-      I.o[k] = s.obstm[fw[k]];
-      I.u[k] = s.vis[vw + gt[k]];
+      I.f[k] = ld_tile<O32>(s.freem, fw[k]);
+      I.o[k] = ld_tile<O32>(s.obstm, fw[k]);
+      I.u[k] = ld_tile<O32>(s.vis, vw + gt[k]);
     }
   } else {
 #pragma unroll
@@ -741,7 +757,13 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
   if (cv) atomicAdd(&L.sc->cnt_vis, cv);
 }
 
-template <int NT, int EPW, typename WT, int KI>
+template <bool O32>
+__device__ __forceinline__ void st_tile(uint64_t* base, uint32_t idx, uint64_t v) {
+  if constexpr (O32) *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(base) + (size_t)(idx << 3)) = v;
+  else base[idx] = v;
+}
+
+template <int NT, int EPW, typename WT, int KI, bool O32 = false>
 __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, WT>& C,
                                             const Items<KI>& I) {
   const uint32_t mt = (uint32_t)s.MT;
@@ -752,10 +774,14 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
     const uint32_t fb = __umul24((uint32_t)C.e * (uint32_t)s.N + (uint32_t)I.a[k], mt) + gt;
     // only obstacle marks can fall on an edge tile's cells beyond the map
     const uint64_t no = I.no[k] & tile_in_grid(s, I.gi[k], I.gj[k]);
-    if (I.nf[k]) s.freem[fb] = I.f[k] | I.nf[k];  // one writer per agent tile
-    if (no) s.obstm[fb] = I.o[k] | no;
-    if (I.nu[k])  // agents' blocks overlap: several lanes may add bits to one tile
-      atomicOr((unsigned long long*)(s.vis + (__umul24((uint32_t)C.e, mt) + gt)), I.nu[k]);
+    if (I.nf[k]) st_tile<O32>(s.freem, fb, I.f[k] | I.nf[k]);  // one writer per agent tile
+    if (no) st_tile<O32>(s.obstm, fb, I.o[k] | no);
+    if (I.nu[k]) {  // agents' blocks overlap: several lanes may add bits to one tile
+      const uint32_t vb = (__umul24((uint32_t)C.e, mt) + gt) << 3;
+      unsigned long long* vp = O32 ? reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s.vis) + (size_t)vb)
+                                   : (unsigned long long*)(s.vis + (__umul24((uint32_t)C.e, mt) + gt));
+      atomicOr(vp, I.nu[k]);
+    }
   }
 }
 
@@ -794,7 +820,7 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int NS, int KN>
+template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -869,10 +895,10 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   __syncthreads();
   Items<KI> I;
   zero_marks<NT, EPW, WT>(s, C);
-  stage<NT, EPW, WT, KI>(s, C, g, /*load_masks=*/false, I);
+  stage<NT, EPW, WT, KI, O32>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
   sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN>(s, C, I);
-  store_tiles<NT, EPW, WT, KI>(s, C, I);
+  store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
     s.free_cnt[e] = L.sc->cnt_free;
@@ -1071,6 +1097,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // beam_kmax, a quarter of a long one (register pressure)
   constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
   constexpr int NSM = (SH::N > 0 && SH::N <= 8) ? SH::N : 0;  // compile-time agent count, if small
+  constexpr bool O32 = SH::N > 0;  // compiled shapes: map byte offsets fit 32 bits (launch_env)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1153,9 +1180,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #pragma unroll
     for (int k = 0; k < KI; ++k) { I.in[k] = false; I.a[k] = I.gi[k] = I.gj[k] = 0; }
 #elif defined(MC_ABL) && MC_ABL == 6
-    stage<NT, EPW, WT, KI>(s, C, g0, false, I);  // timing ablation: grid tiles only
+    stage<NT, EPW, WT, KI, O32>(s, C, g0, false, I);  // timing ablation: grid tiles only
 #else
-    stage<NT, EPW, WT, KI>(s, C, g0, true, I);  // ---- round trip 2 ----
+    stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
 #endif
     // count_nonzero(grid > 0) for percent_covered: kept in a register until
     // the reward (no wait here)
@@ -1199,10 +1226,16 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       }
       const double obs_reward = (double)dsum + (double)c->cnt_vis;
       double r = c->pen + obs_reward;                        // :120,132-151
-      const double pc = (double)fc / (double)numfree;        // :552
       double dt = dthresh0;
       const double thr = (1.0 < dt) ? 1.0 : dt;              // min(done_thresh, 1)
-      const bool covered = thr <= pc;
+      // pc = count/numfree (:552), correctly rounded; thr <= pc.  With thr
+      // == 1 (the default) the test is fc >= numfree exactly (counts are
+      // < 2^24: a quotient below 1 rounds below 1), so the float64 divide
+      // runs only when the threshold or the episode record needs it
+      const bool exact1 = thr == 1.0;
+      double pc = 0.0;
+      if (!exact1) pc = (double)fc / (double)numfree;
+      const bool covered = exact1 ? fc >= (uint32_t)numfree : thr <= pc;
       if (covered) r += s.term;                              // :156-157
       bool done = false;
       if (covered) { dt += s.dincr; done = true; }           // :540-543
@@ -1210,7 +1243,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       reward_out[e] = r;
       done_out[e] = done ? 1 : 0;
       if (done) {  // the episode record (Utils/utils.py:138-141)
-        s.ep_pc[e] = pc;
+        s.ep_pc[e] = exact1 ? (double)fc / (double)numfree : pc;
         s.ep_len[e] = cs;
       }
       s.free_cnt[e] = fc;
@@ -1222,10 +1255,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     __syncthreads();
     STAMP(6);
     if (!L.sc->do_reset) {
-      store_tiles<NT, EPW, WT, KI>(s, C, I);
+      store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK, NSM, SH::KN>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
@@ -1234,12 +1267,12 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK, NSM, SH::KN>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32>(s, C, reset_req ? inj_pos : nullptr);
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
     // obs of the current state only (dec_grid_rl.py:104-107,160)
     Items<KI> I;
-    stage<NT, EPW, WT, KI>(s, C, g0, true, I);
+    stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
     stage_fold<NT, EPW, WT, KI>(s, C, I);
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
@@ -1317,14 +1350,17 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
                      obs, adj)
 #define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
   using Dynamic = Shape<0, 0, 0, 0, 0>;
+  // compiled shapes address the map arrays with 32-bit byte offsets
+  const uint64_t mtb = (uint64_t)s.MT * 8;
+  const bool fits32 = (uint64_t)s.B * s.N * mtb < (1ull << 32) && (uint64_t)s.G * mtb < (1ull << 32);
   using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;    // the bench workload
   using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;  // 360 beams, R=20
   if (epw == 2) {
-    if (narrow && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
+    if (narrow && fits32 && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
   } else if (narrow) {
-    if (nt == 64 && getenv_spec() && ShapeC2::matches(s)) {
+    if (nt == 64 && fits32 && getenv_spec() && ShapeC2::matches(s)) {
       MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2);
       return hipGetLastError();
     }
@@ -1336,7 +1372,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
       default: MC_LAUNCH(1024, 1, uint32_t); break;
     }
   } else {
-    if (nt == 256 && getenv_spec() && ShapeC4::matches(s)) {
+    if (nt == 256 && fits32 && getenv_spec() && ShapeC4::matches(s)) {
       MC_LAUNCH_SH(256, 1, uint64_t, ShapeC4);
       return hipGetLastError();
     }
