@@ -1097,7 +1097,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // beam_kmax, a quarter of a long one (register pressure)
   constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
   constexpr int NSM = (SH::N > 0 && SH::N <= 8) ? SH::N : 0;  // compile-time agent count, if small
-  constexpr bool O32 = SH::N > 0;  // compiled shapes: map byte offsets fit 32 bits (launch_env)
+  // compiled shapes with up to 8 agents: map byte offsets fit 32 bits
+  // (launch_env checks; the C5 shape's maps pass 4 GB)
+  constexpr bool O32 = SH::N > 0 && SH::N <= 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1355,6 +1357,7 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
   const bool fits32 = (uint64_t)s.B * s.N * mtb < (1ull << 32) && (uint64_t)s.G * mtb < (1ull << 32);
   using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;    // the bench workload
   using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;  // 360 beams, R=20
+  using ShapeC5 = Shape<16, 10, 21, 0, 10, 8>;   // 16 agents, dist_reward (4 obs layers)
   if (epw == 2) {
     if (narrow && fits32 && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
@@ -1362,6 +1365,10 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
   } else if (narrow) {
     if (nt == 64 && fits32 && getenv_spec() && ShapeC2::matches(s)) {
       MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2);
+      return hipGetLastError();
+    }
+    if (nt == 128 && getenv_spec() && ShapeC5::matches(s)) {
+      MC_LAUNCH_SH(128, 1, uint32_t, ShapeC5);
       return hipGetLastError();
     }
     switch (nt) {
