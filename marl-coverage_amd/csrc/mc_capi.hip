@@ -521,6 +521,17 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
   E->s.beam_kmax = kmax;
   E->s.beam_kmin = kmin;
   E->s.beam_common = common && !getenv("MARLCOV_BEAM_TABLE") ? 1 : 0;
+  // step-1 cells of the common patterns (lidar.py:52-56: every beam with
+  // K >= 1 reaches its step-1 cell from the free robot cell)
+  uint32_t k1 = 1u << 4;  // the robot cell (step 0)
+  for (int b = 0; b < num_beams; ++b) {
+    const mc::Beam& o = bt[b];
+    if (o.K < 1) continue;
+    const int mv = (o.bits & 1u) ? o.msign : 0;
+    const int dx = o.axis == 0 ? o.sign : mv, dy = o.axis == 0 ? mv : o.sign;
+    k1 |= 1u << (3 * (dx + 1) + (dy + 1));
+  }
+  E->s.beam_k1 = E->s.beam_common && !getenv("MARLCOV_NO_K1") ? k1 : 0u;
   E->beams_set = true;
   return MC_OK;
 }

@@ -129,6 +129,23 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   return L;
 }
 
+// Row planes of 32-bit rows (TW <= 4: every BASELINE config but C4) are
+// agent-interleaved: window row lx of agent a is word lx * N + a.  The rays
+// of one march instruction sit in about N * 8 rows of the slot's agents;
+// interleaved, agent a's rows own the banks = a (mod N) and its consecutive
+// rows are N banks apart, while with agent-major rows, a * (8 TW + 1) + lx,
+// two agents' rows collide whenever a + lx == a' + lx' (mod 32).  A
+// bank-conflict simulation of the C2 march: 2.5x -> 1.5x the conflict-free
+// read cycles; measured C2 9.35 -> 9.25 us.  64-bit rows keep the
+// agent-major order (8-byte words interleaved by 8 agents would fall on 4
+// banks per agent: C4 283 -> 305 us).
+template <typename WT>
+__device__ __forceinline__ int row_step(const State& s) { return sizeof(WT) == 4 ? s.N : 1; }
+template <typename WT>
+__device__ __forceinline__ int row_word(const State& s, int a, int lx) {
+  return sizeof(WT) == 4 ? lx * s.N + a : a * (8 * s.TW + 1) + lx;
+}
+
 // one env slot of the workgroup
 template <int NT, int EPW, typename WT>
 struct Ctx {
@@ -284,13 +301,14 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
       }
       // scatter the tile's 8 row bytes into the row plane (byte tj of rows
       // 8*ti .. 8*ti+7 of the agent's block)
-      const size_t off = (size_t)(I.a[k] * (8 * TW + 1) + 8 * ti[k]) * sizeof(WT) + tj[k];
+      const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * ti[k]) * sizeof(WT) + tj[k];
+      const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
 #pragma unroll
-      for (int r = 0; r < 8; ++r) nb[off + r * sizeof(WT)] = (uint8_t)(nt >> (8 * r));
+      for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
         const uint64_t ft = (load_masks && in) ? (I.f[k] | I.o[k]) : 0ull;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) fb[off + r * sizeof(WT)] = (uint8_t)(ft >> (8 * r));
+        for (int r = 0; r < 8; ++r) fb[off + r * rs] = (uint8_t)(ft >> (8 * r));
       }
     }
   }
@@ -335,23 +353,23 @@ __device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT
 }
 
 // tile (ti, tj) of agent a gathered from a row plane (the inverse scatter):
-// byte r of the tile = byte tj of row r0 + r
+// byte r of the tile = byte tj of word w0 + r * rs (row 8 ti + r; rs = N)
 template <typename WT>
-__device__ __forceinline__ uint64_t gather_tile(const WT* rows, int r0, int tj) {
+__device__ __forceinline__ uint64_t gather_tile(const WT* rows, int w0, int rs, int tj) {
   if constexpr (sizeof(WT) == 4) {
     // v_perm_b32: two rows' byte tj into bytes 0, 1; then two such pairs
     const uint32_t sel = (uint32_t)tj | ((uint32_t)(4 + tj) << 8) | 0x0C0C0000u;
     uint32_t h[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      h[q] = __builtin_amdgcn_perm((uint32_t)rows[r0 + 2 * q + 1], (uint32_t)rows[r0 + 2 * q], sel);
+      h[q] = __builtin_amdgcn_perm((uint32_t)rows[w0 + (2 * q + 1) * rs], (uint32_t)rows[w0 + 2 * q * rs], sel);
     const uint32_t lo = __builtin_amdgcn_perm(h[1], h[0], 0x05040100u);
     const uint32_t hi = __builtin_amdgcn_perm(h[3], h[2], 0x05040100u);
     return (uint64_t)lo | ((uint64_t)hi << 32);
   } else {
     uint64_t t = 0;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) t |= (uint64_t)((rows[r0 + r] >> (8 * tj)) & (WT)0xFF) << (8 * r);
+    for (int r = 0; r < 8; ++r) t |= (uint64_t)((rows[w0 + r * rs] >> (8 * tj)) & (WT)0xFF) << (8 * r);
     return t;
   }
 }
@@ -375,7 +393,7 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
   int gblk = 1;
   if (live && act < 4) {
     const int lx = x + dx - 8 * L.bx[C.sub], ly = y + dy - 8 * L.by[C.sub];
-    gblk = (int)((L.negr[C.sub * (8 * s.TW + 1) + lx] >> ly) & (WT)1);
+    gblk = (int)((L.negr[row_word<WT>(s, C.sub, lx)] >> ly) & (WT)1);
   }
   const int tx = x + dx, ty = y + dy;
   double pen = 0.0;
@@ -410,7 +428,7 @@ __device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT
     DX[i] = (act == 0) - (act == 2);
     DY[i] = (act == 1) - (act == 3);
     const int lx = X[i] + DX[i] - 8 * L.bx[i], ly = Y[i] + DY[i] - 8 * L.by[i];
-    blk[i] = (L.negr[i * (8 * s.TW + 1) + lx] >> ly) & (WT)1;
+    blk[i] = (L.negr[row_word<WT>(s, i, lx)] >> ly) & (WT)1;
   }
   double pen = 0.0;
   uint64_t moved = L.sc->moved;
@@ -470,9 +488,9 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   const int b = R.live ? idx - a * s.nbeams : 0;
   const Beam bm = L.beams[b];
   const int xa = L.x[a], ya = L.y[a];
-  const int row = a * (8 * s.TW + 1) + xa - 8 * L.bx[a];
+  const int row = row_word<WT>(s, a, xa - 8 * L.bx[a]);
   const int col = ya - 8 * L.by[a];
-  constexpr int RB = (int)sizeof(WT) * 64;  // one row in P units
+  const int RB = row_step<WT>(s) * (int)sizeof(WT) * 64;  // one window row in P units
   // the row word's LDS address: P >> 6 is the neg-plane word's address
   // itself (no per-step base add)
   const uint32_t plane = (uint32_t)(uintptr_t)(const lds_char*)(const char*)L.negr;
@@ -505,10 +523,12 @@ __device__ __forceinline__ const WT* ray_word(const Lds<WT>& L, const WT* plane,
 // branches).  Re-marking an already free cell is harmless (OR).
 // `dup`: the lane's previous ray (the adjacent beam) marks the same cell at
 // this step, so this one skips its atomic (near the robot adjacent beams share
-// cells: fewer same-address LDS atomics).  Returns whether the ray marked.
+// cells: fewer same-address LDS atomics).  `premarked`: the cell is one of the
+// step-1 cells sense() marked once per agent (State::beam_k1).  Returns
+// whether the ray marked.
 template <typename WT, int KN>
 __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nrow, WT frow,
-                                         uint32_t sink_m, bool dup, bool frow_valid) {
+                                         uint32_t sink_m, bool dup, bool frow_valid, bool premarked) {
   // KN: a compile-time lower bound of every beam's K (steps k <= KN need no
   // range test)
   const bool on = R.live && (k <= KN || k <= R.K);
@@ -518,16 +538,18 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
   // mark-plane word = row word + a constant; a lane with nothing to mark
   // selects its sink word less that constant (sink_m), so the constant rides
   // in the instruction's offset field.  (Two exec-masked ORs at fixed plane
-  // offsets instead of the select were slower: 10.52 vs 10.04 us at C2.)
+  // offsets instead of the select were slower: 10.52 vs 10.04 us at C2; one
+  // exec-masked OR on the single mark plane gains nothing either: 9.32 vs
+  // 9.15 us.)
   const int delta = (int)(L.fpr - L.negr) * (int)sizeof(WT);
 #if defined(MC_ABL) && MC_ABL == 1
   const uint32_t a = sink_m;  // timing ablation: no marks
 #else
-  const uint32_t a = (on && !dup) ? (R.P >> 6) : sink_m;
+  const uint32_t a = (on && !dup && !premarked) ? (R.P >> 6) : sink_m;
 #endif
   WT* tgt = reinterpret_cast<WT*>((char*)((lds_char*)(uintptr_t)a + delta));  // free or obstacle: the grid tells
   if (frow_valid) {  // dense: most rays skip; an exec-masked OR of the few that mark
-    if (on && !dup) lds_or<WT>(tgt, bit);
+    if (on && !dup && !premarked) lds_or<WT>(tgt, bit);
   } else {
     lds_or<WT>(tgt, bit);
   }
@@ -543,9 +565,21 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
   const Lds<WT>& L = C.L;
   const int N = s.N, TW = s.TW, TW2 = TW * TW;
   if (s.sensor == 0) {
-    // step 0 of every beam is the robot's own (free) cell: mark it once
-    for (int a = C.sub; a < N; a += LPE)
-      lds_or<WT>(&L.fpr[a * (8 * TW + 1) + L.x[a] - 8 * L.bx[a]], (WT)1 << (L.y[a] - 8 * L.by[a]));
+    // step 0 of every beam is the robot's own (free) cell; with common beam
+    // patterns the step-1 cells too (State::beam_k1: every beam reaches its
+    // step-1 cell, lidar.py:52-56).  Marked once per agent -- one lane per
+    // (agent, row x-1 .. x+1) -- instead of once per ray: at step 1 the rays
+    // of an agent crowd three row words, the worst same-address ORs of the
+    // march
+    const uint32_t k1 = s.beam_k1;
+    const int nm = k1 ? 3 * N : N;
+    for (int m = C.sub; m < nm; m += LPE) {
+      const int a = k1 ? m / 3 : m;
+      const int dx = k1 ? m - 3 * a - 1 : 0;
+      const uint32_t b3 = k1 ? (k1 >> (3 * (dx + 1))) & 7u : 2u;  // cells y-1, y, y+1
+      const int lx = L.x[a] - 8 * L.bx[a] + dx, ly = L.y[a] - 8 * L.by[a] - 1;  // ly >= H >= 1
+      if (b3) lds_or<WT>(&L.fpr[row_word<WT>(s, a, lx)], (WT)b3 << ly);
+    }
     WT* sink = L.sink + (threadIdx.x & 63);
     const uint32_t sink_m = (uint32_t)(uintptr_t)(const lds_char*)(const char*)sink -
                             (uint32_t)((L.fpr - L.negr) * (int)sizeof(WT));
@@ -595,7 +629,8 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
             for (int j = 0; j < RPL; ++j) {
               const bool dup = dense && prev_on && q[j].P == prev_p;
               prev_p = q[j].P;
-              prev_on = ray_mark<WT, KN>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink_m, dup, dense);
+              prev_on = ray_mark<WT, KN>(L, q[j], k0 + u, nr[u][j], fr[u][j], sink_m, dup, dense,
+                                         k1 != 0 && k0 + u == 1);
               ray_advance(q[j], k0 + u);
             }
           }
@@ -637,8 +672,7 @@ __device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, 
     if (idx < items) {
       const int a = udiv(idx, s.mg_TW2), rem = idx - a * TW2;
       const int ti = udiv(rem, s.mg_TW), tj = rem - ti * TW;
-      const int r0 = a * (8 * TW + 1) + 8 * ti;
-      const uint64_t m = gather_tile<WT>(L.fpr, r0, tj);
+      const uint64_t m = gather_tile<WT>(L.fpr, row_word<WT>(s, a, 8 * ti), row_step<WT>(s), tj);
       I.mf[k] = m & ~I.n[k];
       I.mo[k] = m & I.n[k];
       L.fp[idx] = I.mf[k];

@@ -78,6 +78,11 @@ struct State {
   // grid's border (an obstacle, so the march ends there): the march needs no
   // beam_bits load (mc_set_beam_table checks this on the host)
   int beam_common;
+  // beam_common: the cells every beam visits at step 1 (always reached: step 0
+  // is the robot's own free cell), and the robot cell, as a 3x3 mask around
+  // the robot (bit 3*(dx+1) + (dy+1)); the march marks them once per agent
+  // instead of once per ray (0 = no premark, the march marks step 1)
+  uint32_t beam_k1;
   int32_t* env_grid;
   int32_t* pos;
   uint64_t* moved;
