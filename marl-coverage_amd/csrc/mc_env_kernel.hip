@@ -183,7 +183,9 @@ struct Items {
   uint64_t f[KI], o[KI], u[KI];     // old free / obst / union tiles (raw loads)
   uint64_t nf[KI], no[KI], nu[KI];  // newly set bits
   uint64_t mf[KI], mo[KI];          // lidar: this step's free / obstacle marks (gather_marks)
-  uint64_t n[KI];                   // grid < 0 tiles (outside the map: all ones)
+  uint64_t n[KI];                   // grid < 0 tiles (raw load; outside the map: all ones after stage_scatter)
+  uint64_t p[KI];                   // grid > 0 tiles (square sensor)
+  int ti[KI], tj[KI];               // tile within the agent's block
   bool masks;                       // f / o / u were loaded (else known zero)
 };
 
@@ -217,9 +219,63 @@ __device__ __forceinline__ uint64_t ld_tile(const uint64_t* base, uint32_t idx) 
 // --------------------------------------------------------------------------
 // stage: one round trip for every staged tile (masks known zero after reset)
 // --------------------------------------------------------------------------
-template <int NT, int EPW, typename WT, int KI, bool O32 = false>
-__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, int g,
-                                      bool load_masks, Items<KI>& I) {
+// Compiled shapes with at most 8 robots and one wave per workgroup: the
+// robots' pre-move cells and actions are broadcast to every lane of the slot
+// by v_readlane right after round trip 1 (no LDS round trip, no barrier), so
+// the tile-block origins of round trip 2 and the moves come from registers.
+template <int NS>
+struct Front {
+  uint32_t xy[NS > 0 ? NS : 1];  // pre-move cell, x | y << 16
+  int act[NS > 0 ? NS : 1];
+  int bx[NS > 0 ? NS : 1], by[NS > 0 ? NS : 1];  // tile-block origins
+};
+
+// R[a] for a runtime index a < NS, as a select chain (the empty asm keeps
+// the compiler from folding the chain back into an indexed scratch array)
+template <int NS>
+__device__ __forceinline__ int pick(const int (&R)[NS], int a) {
+  int v = R[0];
+#pragma unroll
+  for (int i = 1; i < NS; ++i) {
+    v = a == i ? R[i] : v;
+    asm volatile("" : "+v"(v));
+  }
+  return v;
+}
+
+// the value v of lane lane0 + i of this lane's slot, read with wave-uniform
+// lane indices (v_readlane) and selected by slot
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ int slot_lane(const Ctx<NT, EPW, WT>& C, int v, int i) {
+  static_assert(NT == 64, "one wave per workgroup");
+  if constexpr (EPW == 1) return rdlane(v, i);
+  else {
+    static_assert(EPW == 2, "two slots per wave");
+    const int lo = rdlane(v, i), hi = rdlane(v, 32 + i);
+    return C.lane0 ? hi : lo;
+  }
+}
+
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void front_regs(const State& s, const Ctx<NT, EPW, WT>& C, int x, int y, int act,
+                                           Front<NS>& F) {
+  const int xy = (int)((uint32_t)x | ((uint32_t)y << 16));
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    F.xy[i] = (uint32_t)slot_lane(C, xy, i);
+    F.act[i] = slot_lane(C, act, i);
+    F.bx[i] = ((int)(F.xy[i] & 0xFFFFu) - s.H - 1) >> 3;  // arithmetic shift: floor
+    F.by[i] = ((int)(F.xy[i] >> 16) - s.H - 1) >> 3;
+  }
+}
+
+// round trip 2, issue: addresses, then every load of the lane back to back
+// with no exec-mask branches (tiles outside the map read tile 0 and are
+// replaced in stage_scatter).  NS > 0: block origins from F (registers),
+// else from LDS (L.bx / L.by, written after round trip 1).
+template <int NT, int EPW, typename WT, int KI, bool O32 = false, int NS = 0>
+__device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT>& C, int g,
+                                           bool load_masks, Items<KI>& I, const Front<NS>* F = nullptr) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const Lds<WT>& L = C.L;
   const int TW = s.TW, TW2 = TW * TW;
@@ -227,11 +283,10 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   const uint32_t mt = (uint32_t)s.MT;
   const uint32_t gb = __umul24((uint32_t)g, mt);  // this env's grid in the pool (tiles)
   const bool square = s.sensor == 1;
-  uint64_t n[KI], p[KI];
   // 32-bit word indices (mc_create bounds every map array below 2^32 words);
   // products of 24-bit factors are single v_mul_u32_u24
   uint32_t gt[KI], fw[KI];
-  int ti[KI], tj[KI], bxa[KI], bya[KI];
+  int bxa[KI], bya[KI];
   const uint32_t eN = (uint32_t)C.e * (uint32_t)s.N;
   // every item's block origin read first (one LDS round trip for all items)
 #pragma unroll
@@ -240,18 +295,21 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     const bool it = idx < items;
     const int a = it ? udiv(idx, s.mg_TW2) : 0;
     const int rem = idx - a * TW2;
-    ti[k] = udiv(rem, s.mg_TW);
-    tj[k] = rem - ti[k] * TW;
+    I.ti[k] = udiv(rem, s.mg_TW);
+    I.tj[k] = rem - I.ti[k] * TW;
     I.a[k] = a;
-    bxa[k] = L.bx[a];
-    bya[k] = L.by[a];
+    if constexpr (NS > 0) {
+      bxa[k] = pick<NS>(F->bx, a);
+      bya[k] = pick<NS>(F->by, a);
+    } else {
+      bxa[k] = L.bx[a];
+      bya[k] = L.by[a];
+    }
   }
-  // addresses, then every load of the lane back to back with no exec-mask
-  // branches (tiles outside the map read tile 0 and are replaced)
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const int idx = C.sub + k * LPE;
-    const int gi = bxa[k] + ti[k], gj = bya[k] + tj[k];
+    const int gi = bxa[k] + I.ti[k], gj = bya[k] + I.tj[k];
     I.gi[k] = gi;
     I.gj[k] = gj;
     I.in[k] = (idx < items) & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
@@ -263,10 +321,10 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   // tiles (needed from the merge on) stay in flight meanwhile (loads return
   // in order; the compiler waits only for what each use needs)
 #pragma unroll
-  for (int k = 0; k < KI; ++k) n[k] = ld_tile<O32>(s.grid_neg, gb + gt[k]);
+  for (int k = 0; k < KI; ++k) I.n[k] = ld_tile<O32>(s.grid_neg, gb + gt[k]);
   if (square) {
 #pragma unroll
-    for (int k = 0; k < KI; ++k) p[k] = ld_tile<O32>(s.grid_pos, gb + gt[k]);
+    for (int k = 0; k < KI; ++k) I.p[k] = ld_tile<O32>(s.grid_pos, gb + gt[k]);
   }
   if (load_masks) {
 #pragma unroll
@@ -280,6 +338,16 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     for (int k = 0; k < KI; ++k) I.f[k] = I.o[k] = I.u[k] = 0;
   }
   I.masks = load_masks;
+}
+
+// round trip 2, landing: the grid tiles into the row planes (and the tile
+// planes for the square sensor)
+template <int NT, int EPW, typename WT, int KI>
+__device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  const int items = s.N * s.TW * s.TW;
+  const bool square = s.sensor == 1;
 #ifdef MC_STAMPS
   STAMP(11);  // loads issued
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -293,25 +361,32 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
     const bool in = I.in[k];
     const int idx = C.sub + k * LPE;
     if (idx < items) {
-      const uint64_t nt = in ? n[k] : ~0ull;  // outside the map: blocked (isInBounds)
+      const uint64_t nt = in ? I.n[k] : ~0ull;  // outside the map: blocked (isInBounds)
       I.n[k] = nt;
       if (square) {
         L.neg[idx] = nt;
-        L.pos[idx] = in ? p[k] : 0ull;
+        L.pos[idx] = in ? I.p[k] : 0ull;
       }
       // scatter the tile's 8 row bytes into the row plane (byte tj of rows
       // 8*ti .. 8*ti+7 of the agent's block)
-      const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * ti[k]) * sizeof(WT) + tj[k];
+      const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
-        const uint64_t ft = (load_masks && in) ? (I.f[k] | I.o[k]) : 0ull;
+        const uint64_t ft = (I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
 #pragma unroll
         for (int r = 0; r < 8; ++r) fb[off + r * rs] = (uint8_t)(ft >> (8 * r));
       }
     }
   }
+}
+
+template <int NT, int EPW, typename WT, int KI, bool O32 = false>
+__device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C, int g,
+                                      bool load_masks, Items<KI>& I) {
+  stage_load<NT, EPW, WT, KI, O32>(s, C, g, load_masks, I);
+  stage_scatter<NT, EPW, WT, KI>(s, C, I);
 }
 
 // old mask tiles of item k (zero outside the map, where nothing is stored)
@@ -451,6 +526,46 @@ __device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT
     for (int i = 0; i < NS; ++i) {
       L.x[i] = X[i];
       L.y[i] = Y[i];
+    }
+    L.sc->pen = pen;
+    L.sc->moved = moved;
+  }
+}
+
+// Moves from registers (Front): robot i's target-cell bit (grid < 0 or out of
+// bounds) was loaded by lane lane0 + i next to round trip 2 and is shared by
+// a ballot; every lane of the slot replays the robot-order loop; lane 0
+// publishes the result.  Same semantics as moves_regs.
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void moves_front(const State& s, const Ctx<NT, EPW, WT>& C, const Front<NS>& F,
+                                            bool tgt_blk, uint64_t moved, double pen_unit) {
+  const Lds<WT>& L = C.L;
+  const uint64_t bm = slot_ballot(C, C.sub < NS && tgt_blk);  // bit i: robot i's target is blocked
+  uint32_t XY[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) XY[i] = F.xy[i];
+  double pen = 0.0;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int act = F.act[i];
+    const bool acts = act <= 3;  // not 0..3: no updateRobotPos call, no penalty
+    const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+    const uint32_t t = (uint32_t)((int)(XY[i] & 0xFFFFu) + dx) | ((uint32_t)((int)(XY[i] >> 16) + dy) << 16);
+    bool occ = false;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) occ |= XY[j] == t;  // live positions (:186,190-199,310)
+    const bool ok = acts && !((bm >> i) & 1ull) && !occ;
+    if (ok) {
+      XY[i] = t;
+      moved |= 1ull << i;
+    }
+    if (acts && !ok) pen += pen_unit;  // reward += -collision_penalty (:203)
+  }
+  if (C.sub == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      L.x[i] = (int)(XY[i] & 0xFFFFu);
+      L.y[i] = (int)(XY[i] >> 16);
     }
     L.sc->pen = pen;
     L.sc->moved = moved;
@@ -1134,6 +1249,13 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // compiled shapes with up to 8 agents: map byte offsets fit 32 bits
   // (launch_env checks; the C5 shape's maps pass 4 GB)
   constexpr bool O32 = SH::N > 0 && SH::N <= 8;
+  // register front (front_regs / moves_front): compiled agent count <= 8,
+  // one wave per workgroup; MC_NO_FRONT builds the LDS front (A/B)
+#ifdef MC_NO_FRONT
+  constexpr bool FRONT = false;
+#else
+  constexpr bool FRONT = NSM > 0 && NT == 64;
+#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1218,7 +1340,23 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #elif defined(MC_ABL) && MC_ABL == 6
     stage<NT, EPW, WT, KI, O32>(s, C, g0, false, I);  // timing ablation: grid tiles only
 #else
-    stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
+    if constexpr (FRONT) {
+      // ---- round trip 2, issue: the robots' target-cell grid tiles first
+      // (the moves wait only for them), then every staged tile; block
+      // origins and moves from registers (front_regs)
+      Front<NSM> F;
+      front_regs<NT, EPW, WT, NSM>(s, C, p0.x, p0.y, act, F);
+      const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+      const int tx = p0.x + dx, ty = p0.y + dy;
+      const bool inb = (unsigned)tx < (unsigned)s.Wp && (unsigned)ty < (unsigned)s.Lp;
+      const uint64_t tt = ld_tile<O32>(s.grid_neg, __umul24((uint32_t)g0, (uint32_t)s.MT) +
+                                                       tile_index(s.TCS, inb ? tx >> 3 : 0, inb ? ty >> 3 : 0));
+      stage_load<NT, EPW, WT, KI, O32, NSM>(s, C, g0, true, I, &F);
+      moves_front<NT, EPW, WT, NSM>(s, C, F, !inb || ((tt >> tile_bit(tx, ty)) & 1ull), moved0, -s.pen);
+      stage_scatter<NT, EPW, WT, KI>(s, C, I);
+    } else {
+      stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
+    }
 #endif
     // count_nonzero(grid > 0) for percent_covered: kept in a register until
     // the reward (no wait here)
@@ -1235,10 +1373,12 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #else
     // (the same loop on the scalar unit, robots read by v_readlane, was
     // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
-    if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
-    else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
+    if constexpr (!FRONT) {  // (FRONT: moved during round trip 2)
+      if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
+      else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
+      __syncthreads();
+    }
 #endif
-    __syncthreads();
     STAMP(3);
     sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN>(s, C, I);
 #endif
