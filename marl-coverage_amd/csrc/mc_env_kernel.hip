@@ -97,7 +97,7 @@ template <typename WT>
 __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   Lds<WT> L;
   const int tiles = s.N * s.TW * s.TW;
-  const int rows = s.N * (8 * s.TW + 1);
+  const int rows = row_plane_words(s.N, s.TW, (int)sizeof(WT));
   uint64_t* p = reinterpret_cast<uint64_t*>(smem);
   L.neg = p;
   L.pos = p + tiles;
@@ -140,10 +140,10 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
 // agent-major order (8-byte words interleaved by 8 agents would fall on 4
 // banks per agent: C4 283 -> 305 us).
 template <typename WT>
-__device__ __forceinline__ int row_step(const State& s) { return sizeof(WT) == 4 ? s.N : 1; }
+__device__ __forceinline__ int row_step(const State& s) { return sizeof(WT) == 4 ? (s.N | 1) : 1; }
 template <typename WT>
 __device__ __forceinline__ int row_word(const State& s, int a, int lx) {
-  return sizeof(WT) == 4 ? lx * s.N + a : a * (8 * s.TW + 1) + lx;
+  return sizeof(WT) == 4 ? lx * (s.N | 1) + a : a * (8 * s.TW + 1) + lx;
 }
 
 // one env slot of the workgroup
@@ -371,8 +371,12 @@ __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW,
       // 8*ti .. 8*ti+7 of the agent's block)
       const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
+#if defined(MC_ABL) && MC_ABL == 13
+      // timing ablation: no row-plane scatter (the march sees an empty grid)
+#else
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
+#endif
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
         const uint64_t ft = (I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
 #pragma unroll
@@ -422,7 +426,7 @@ template <int NT, int EPW, typename WT>
 __device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   if (s.sensor != 0) return;
-  for (int r = C.sub; r < s.N * (8 * s.TW + 1); r += LPE) {
+  for (int r = C.sub; r < row_plane_words(s.N, s.TW, (int)sizeof(WT)); r += LPE) {
     C.L.fpr[r] = 0;
   }
 }
@@ -1212,17 +1216,40 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
   const int e_first = blockIdx.x * EPW;  // the wave's first env
   uint32_t* out = reinterpret_cast<uint32_t*>(obs_out + (size_t)e_first * (NB * EE));
   const int lane = (int)(threadIdx.x & 63);
-#pragma unroll
-  for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + lane;
-    const int es = EPW == 1 ? 0 : d / DPE;  // env slot of dword d
-    const int i = 4 * (d - es * DPE);       // its first bit within that env's stream
-    const int jb = i / EE, o = i - jb * EE;
+  // three dwords per lane when an env's run is whole triples and the wave's
+  // triples fit 64 lanes (C2: 25 per env): one pair of ds_bpermutes and one
+  // global_store_dwordx3 per lane; a triple's 12 bits span at most two crops
+  constexpr int TPE = DPE / 3;  // dword triples per env
+  constexpr bool X3 = DPE % 3 == 0 && EPW * TPE <= 64 && EE >= 12;
+  if constexpr (X3) {
+    const int es = EPW == 1 ? 0 : lane / TPE;  // env slot of the lane's triple
+    const int b0 = 12 * (lane - es * TPE);     // its first bit within that env's stream
+    const int jb = b0 / EE, o = b0 - jb * EE;
     const int src = es * LPE + jb;
     const uint32_t w0 = (uint32_t)__shfl((int)crop, src);
     const uint32_t w1 = (uint32_t)__shfl((int)crop, src + 1 < 64 ? src + 1 : src);
-    const uint32_t nib = ((w0 | (w1 << EE)) >> o) & 0xFu;
-    if (d < D && e_first + es < s.B) out[d] = (nib * 0x00204081u) & 0x01010101u;
+    const uint32_t bits = (uint32_t)((((uint64_t)w1 << EE) | w0) >> o);
+    if (lane < EPW * TPE && e_first + es < s.B) {
+      typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+      u32x3 v;
+      v.x = ((bits & 0xFu) * 0x00204081u) & 0x01010101u;
+      v.y = (((bits >> 4) & 0xFu) * 0x00204081u) & 0x01010101u;
+      v.z = (((bits >> 8) & 0xFu) * 0x00204081u) & 0x01010101u;
+      *reinterpret_cast<u32x3*>(out + 3 * lane) = v;
+    }
+  } else {
+#pragma unroll
+    for (int d0 = 0; d0 < D; d0 += 64) {
+      const int d = d0 + lane;
+      const int es = EPW == 1 ? 0 : d / DPE;  // env slot of dword d
+      const int i = 4 * (d - es * DPE);       // its first bit within that env's stream
+      const int jb = i / EE, o = i - jb * EE;
+      const int src = es * LPE + jb;
+      const uint32_t w0 = (uint32_t)__shfl((int)crop, src);
+      const uint32_t w1 = (uint32_t)__shfl((int)crop, src + 1 < 64 ? src + 1 : src);
+      const uint32_t nib = ((w0 | (w1 << EE)) >> o) & 0xFu;
+      if (d < D && e_first + es < s.B) out[d] = (nib * 0x00204081u) & 0x01010101u;
+    }
   }
 }
 

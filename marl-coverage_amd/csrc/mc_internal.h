@@ -135,11 +135,18 @@ __host__ __device__ constexpr uint32_t magic_div(uint32_t d) {
   return d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d);
 }
 
+// Words of one row plane of the env kernel (mc_env_kernel.hip row_word):
+// 32-bit rows are agent-interleaved with an odd stride N | 1 (row lx of agent
+// a is word lx * (N | 1) + a), 64-bit rows agent-major, 8*TW + 1 apart.
+__host__ __device__ inline int row_plane_words(int N, int TW, int rowbytes) {
+  return rowbytes == 4 ? 8 * TW * (N | 1) : N * (8 * TW + 1);
+}
+
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
 // rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
 __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes) {
   size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
-  b += (((size_t)3 * N * (8 * TW + 1) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
+  b += (((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
   b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
   b += 64;                                             // scalars
