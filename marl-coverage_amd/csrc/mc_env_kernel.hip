@@ -206,6 +206,13 @@ __device__ __forceinline__ void lds_or(WT* p, WT v) {
 // less than the extra reads cost (measured: 10.9 vs 10.0 us at C2).
 __device__ __forceinline__ bool dense_beams(const State& s) { return s.sensor == 0 && s.nbeams >= 64; }
 
+// tile_index (mc_internal.h) for non-negative tile coordinates below 2^24:
+// one full-rate v_mul_u32_u24 instead of a quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t tile_index24(int TCS, int ti, int tj) {
+  return ((__umul24((uint32_t)(ti >> 2), (uint32_t)TCS) + (uint32_t)(tj >> 2)) << 4) |
+         (uint32_t)((ti & 3) << 2) | (uint32_t)(tj & 3);
+}
+
 // tile idx of a map array.  O32: the launcher checked that every byte offset
 // of the arrays fits 32 bits, so the address is the array base (uniform,
 // SGPRs) plus a 32-bit offset (one VGPR: global_load's saddr form, no
@@ -256,14 +263,37 @@ __device__ __forceinline__ int slot_lane(const Ctx<NT, EPW, WT>& C, int v, int i
   }
 }
 
+// QUAD (NS divides 4): round trip 1 loaded robot sub % NS into every lane,
+// so lanes 4q + i of every quad hold robot i and one DPP quad_perm broadcast
+// (full rate, no LDS) gives every lane robot i's value
+template <int NS>
+struct FrontQuad {
+  static constexpr bool ok = NS > 0 && 4 % NS == 0;
+};
+
+template <int NS>
+__device__ __forceinline__ int quad_bcast(int v, int i) {  // i: a constant once unrolled
+  switch (i) {  // quad_perm [i, i, i, i]
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);
+  }
+}
+
 template <int NT, int EPW, typename WT, int NS>
 __device__ __forceinline__ void front_regs(const State& s, const Ctx<NT, EPW, WT>& C, int x, int y, int act,
                                            Front<NS>& F) {
   const int xy = (int)((uint32_t)x | ((uint32_t)y << 16));
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
-    F.xy[i] = (uint32_t)slot_lane(C, xy, i);
-    F.act[i] = slot_lane(C, act, i);
+    if constexpr (FrontQuad<NS>::ok) {
+      F.xy[i] = (uint32_t)quad_bcast<NS>(xy, i);
+      F.act[i] = quad_bcast<NS>(act, i);
+    } else {
+      F.xy[i] = (uint32_t)slot_lane(C, xy, i);
+      F.act[i] = slot_lane(C, act, i);
+    }
     F.bx[i] = ((int)(F.xy[i] & 0xFFFFu) - s.H - 1) >> 3;  // arithmetic shift: floor
     F.by[i] = ((int)(F.xy[i] >> 16) - s.H - 1) >> 3;
   }
@@ -313,7 +343,7 @@ __device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT
     I.gi[k] = gi;
     I.gj[k] = gj;
     I.in[k] = (idx < items) & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
-    gt[k] = tile_index(s.TCS, I.in[k] ? gi : 0, I.in[k] ? gj : 0);
+    gt[k] = tile_index24(s.TCS, I.in[k] ? gi : 0, I.in[k] ? gj : 0);
     fw[k] = __umul24(eN + (uint32_t)I.a[k], mt) + gt[k];
   }
   const uint32_t vw = __umul24((uint32_t)C.e, mt);
@@ -542,23 +572,38 @@ __device__ __forceinline__ void moves_regs(const State& s, const Ctx<NT, EPW, WT
 // publishes the result.  Same semantics as moves_regs.
 template <int NT, int EPW, typename WT, int NS>
 __device__ __forceinline__ void moves_front(const State& s, const Ctx<NT, EPW, WT>& C, const Front<NS>& F,
-                                            bool tgt_blk, uint64_t moved, double pen_unit) {
+                                            bool tgt_blk, uint32_t txy, int act_own, uint64_t moved,
+                                            double pen_unit) {
   const Lds<WT>& L = C.L;
-  const uint64_t bm = slot_ballot(C, C.sub < NS && tgt_blk);  // bit i: robot i's target is blocked
+  // QUAD: every lane holds its quad's robot (sub % NS): its packed target
+  // and flags (bit 0 blocked, bit 1 acts) go to the loop by quad_perm
+  const int fl = (tgt_blk ? 1 : 0) | (act_own <= 3 ? 2 : 0);
+  uint64_t bm = 0;
+  if constexpr (!FrontQuad<NS>::ok) bm = slot_ballot(C, C.sub < NS && tgt_blk);  // bit i: robot i's target is blocked
   uint32_t XY[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) XY[i] = F.xy[i];
   double pen = 0.0;
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
-    const int act = F.act[i];
-    const bool acts = act <= 3;  // not 0..3: no updateRobotPos call, no penalty
-    const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
-    const uint32_t t = (uint32_t)((int)(XY[i] & 0xFFFFu) + dx) | ((uint32_t)((int)(XY[i] >> 16) + dy) << 16);
+    bool acts, blk;
+    uint32_t t;
+    if constexpr (FrontQuad<NS>::ok) {
+      const int fi = quad_bcast<NS>(fl, i);
+      acts = (fi & 2) != 0;
+      blk = (fi & 1) != 0;
+      t = (uint32_t)quad_bcast<NS>((int)txy, i);
+    } else {
+      const int act = F.act[i];
+      acts = act <= 3;  // not 0..3: no updateRobotPos call, no penalty
+      blk = (bm >> i) & 1ull;
+      const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+      t = (uint32_t)((int)(XY[i] & 0xFFFFu) + dx) | ((uint32_t)((int)(XY[i] >> 16) + dy) << 16);
+    }
     bool occ = false;
 #pragma unroll
     for (int j = 0; j < NS; ++j) occ |= XY[j] == t;  // live positions (:186,190-199,310)
-    const bool ok = acts && !((bm >> i) & 1ull) && !occ;
+    const bool ok = acts && !blk && !occ;
     if (ok) {
       XY[i] = t;
       moved |= 1ull << i;
@@ -923,7 +968,7 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     if (!I.in[k]) continue;
-    const uint32_t gt = tile_index(s.TCS, I.gi[k], I.gj[k]);
+    const uint32_t gt = tile_index24(s.TCS, I.gi[k], I.gj[k]);
     const uint32_t fb = __umul24((uint32_t)C.e * (uint32_t)s.N + (uint32_t)I.a[k], mt) + gt;
     // only obstacle marks can fall on an edge tile's cells beyond the map
     const uint64_t no = I.no[k] & tile_in_grid(s, I.gi[k], I.gj[k]);
@@ -1305,7 +1350,9 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // ---- round trip 1: positions, actions, scalars, beam table.  Every load
   // is issued (unpredicated, clamped addresses) before any result is used:
   // one round trip, not one per branch.
-  const int ag = C.sub < N ? C.sub : 0;
+  // (register front with QUAD: every lane loads robot sub % N, so each quad
+  // holds all robots; other lanes of other builds read robot 0)
+  const int ag = (FRONT && FrontQuad<NSM>::ok) ? (C.sub & (N - 1)) : (C.sub < N ? C.sub : 0);
   // absent inputs read a harmless valid byte instead (no branch, no wait)
   const uint8_t* ab = is_step ? actions + (size_t)e * N : reinterpret_cast<const uint8_t*>(s.pos);
   const uint8_t* mb = env_mask != nullptr ? env_mask + e : reinterpret_cast<const uint8_t*>(s.pos);
@@ -1377,9 +1424,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       const int tx = p0.x + dx, ty = p0.y + dy;
       const bool inb = (unsigned)tx < (unsigned)s.Wp && (unsigned)ty < (unsigned)s.Lp;
       const uint64_t tt = ld_tile<O32>(s.grid_neg, __umul24((uint32_t)g0, (uint32_t)s.MT) +
-                                                       tile_index(s.TCS, inb ? tx >> 3 : 0, inb ? ty >> 3 : 0));
+                                                       tile_index24(s.TCS, inb ? tx >> 3 : 0, inb ? ty >> 3 : 0));
       stage_load<NT, EPW, WT, KI, O32, NSM>(s, C, g0, true, I, &F);
-      moves_front<NT, EPW, WT, NSM>(s, C, F, !inb || ((tt >> tile_bit(tx, ty)) & 1ull), moved0, -s.pen);
+      moves_front<NT, EPW, WT, NSM>(s, C, F, !inb || ((tt >> tile_bit(tx, ty)) & 1ull),
+                                    (uint32_t)tx | ((uint32_t)ty << 16), act, moved0, -s.pen);
       stage_scatter<NT, EPW, WT, KI>(s, C, I);
     } else {
       stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
