@@ -284,9 +284,11 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   ALLOC(s.env_grid, int32_t, B);
   ALLOC(s.pos, int32_t, B * N * 2);
   ALLOC(s.moved, uint64_t, B);
-  ALLOC(s.freem, uint64_t, B * N * mw);
-  ALLOC(s.obstm, uint64_t, B * N * mw);
-  ALLOC(s.vis, uint64_t, B * mw);
+  // one extra tile past each mask array stays zero: the env kernel's staged
+  // tiles outside the map read it (no select on the loaded value)
+  ALLOC(s.freem, uint64_t, B * N * mw + 1);
+  ALLOC(s.obstm, uint64_t, B * N * mw + 1);
+  ALLOC(s.vis, uint64_t, B * mw + 1);
   ALLOC(s.free_cnt, uint32_t, B);
   ALLOC(s.vis_cnt, uint32_t, B);
   ALLOC(s.currstep, int32_t, B);

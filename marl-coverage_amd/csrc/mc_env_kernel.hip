@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "mc_device.h"
 
@@ -69,6 +70,7 @@ struct Scal {
   int32_t do_reset;
   int32_t pad_;
   uint64_t dist_hit;   // dist_reward: agents whose witness cell got closer than M
+  uint64_t zero;       // always 0: the merge's dedup reads it for agents whose block misses the tile
 };
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 
@@ -213,6 +215,20 @@ __device__ __forceinline__ uint32_t tile_index24(int TCS, int ti, int tj) {
          (uint32_t)((ti & 3) << 2) | (uint32_t)(tj & 3);
 }
 
+// element i of a per-env / per-agent array.  O32: every such array's byte
+// offsets fit 32 bits (launch-checked with the maps), so the address is the
+// uniform base plus a 32-bit offset (global_* saddr form, no 64-bit address
+// arithmetic per access)
+template <bool O32, typename T>
+__device__ __forceinline__ T& el(T* base, uint32_t i) {
+  if constexpr (O32) {
+    using B = std::conditional_t<std::is_const_v<T>, const char, char>;  // keep const, stay a global pointer
+    return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + (size_t)(i * (uint32_t)sizeof(T)));
+  } else {
+    return base[i];
+  }
+}
+
 // tile idx of a map array.  O32: the launcher checked that every byte offset
 // of the arrays fits 32 bits, so the address is the array base (uniform,
 // SGPRs) plus a 32-bit offset (one VGPR: global_load's saddr form, no
@@ -315,9 +331,11 @@ __device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT
   const bool square = s.sensor == 1;
   // 32-bit word indices (mc_create bounds every map array below 2^32 words);
   // products of 24-bit factors are single v_mul_u32_u24
-  uint32_t gt[KI], fw[KI];
+  uint32_t gt[KI], fw[KI], vk[KI];
   int bxa[KI], bya[KI];
   const uint32_t eN = (uint32_t)C.e * (uint32_t)s.N;
+  const uint32_t vw = __umul24((uint32_t)C.e, mt);
+  const uint32_t zf = (uint32_t)s.B * (uint32_t)s.N * mt, zv = (uint32_t)s.B * mt;  // the zero tiles
   // every item's block origin read first (one LDS round trip for all items)
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
@@ -344,9 +362,10 @@ __device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT
     I.gj[k] = gj;
     I.in[k] = (idx < items) & ((unsigned)gi < (unsigned)s.TR) & ((unsigned)gj < (unsigned)s.TC);
     gt[k] = tile_index24(s.TCS, I.in[k] ? gi : 0, I.in[k] ? gj : 0);
-    fw[k] = __umul24(eN + (uint32_t)I.a[k], mt) + gt[k];
+    // tiles outside the map read the mask arrays' zero tile (mc_create)
+    fw[k] = I.in[k] ? __umul24(eN + (uint32_t)I.a[k], mt) + gt[k] : zf;
+    vk[k] = I.in[k] ? vw + gt[k] : zv;
   }
-  const uint32_t vw = __umul24((uint32_t)C.e, mt);
   // grid tiles first: the moves and the march need only them, so the mask
   // tiles (needed from the merge on) stay in flight meanwhile (loads return
   // in order; the compiler waits only for what each use needs)
@@ -361,7 +380,7 @@ __device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT
     for (int k = 0; k < KI; ++k) {
       I.f[k] = ld_tile<O32>(s.freem, fw[k]);
       I.o[k] = ld_tile<O32>(s.obstm, fw[k]);
-      I.u[k] = ld_tile<O32>(s.vis, vw + gt[k]);
+      I.u[k] = ld_tile<O32>(s.vis, vk[k]);
     }
   } else {
 #pragma unroll
@@ -423,14 +442,14 @@ __device__ __forceinline__ void stage(const State& s, const Ctx<NT, EPW, WT>& C,
   stage_scatter<NT, EPW, WT, KI>(s, C, I);
 }
 
-// old mask tiles of item k (zero outside the map, where nothing is stored)
+// old mask tiles of item k (zero outside the map, where nothing is stored:
+// such items loaded the arrays' zero tile; without mask loads they are 0)
 template <int KI>
 __device__ __forceinline__ void old_tiles(const Items<KI>& I, int k, uint64_t& f, uint64_t& o,
                                           uint64_t& u) {
-  const bool m = I.masks && I.in[k];
-  f = m ? I.f[k] : 0;
-  o = m ? I.o[k] : 0;
-  u = m ? I.u[k] : 0;
+  f = I.f[k];
+  o = I.o[k];
+  u = I.u[k];
 }
 
 // the old free / obstacle tiles into LDS (obs of an env that does not step)
@@ -914,16 +933,17 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 #endif
         // marks of lower-index agents in this tile: every read issued
         // unconditionally (own tile when unused), no loop-carried branch
+        // (an agent whose block misses the tile, or b >= a, reads the
+        // slot's zero word)
         uint64_t t[NS > 1 ? NS - 1 : 1];
-        bool use[NS > 1 ? NS - 1 : 1];
 #pragma unroll
         for (int b = 0; b < NS - 1; ++b) {
           const int bi = gi - BX[b], bj = gj - BY[b];
-          use[b] = b < a && (unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW;
-          t[b] = L.fp[use[b] ? (b * TW + bi) * TW + bj : idx];
+          const bool use = b < a && (unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW;
+          t[b] = *(use ? &L.fp[(b * TW + bi) * TW + bj] : &L.sc->zero);
         }
 #pragma unroll
-        for (int b = 0; b < NS - 1; ++b) cand &= use[b] ? ~t[b] : ~0ull;
+        for (int b = 0; b < NS - 1; ++b) cand &= ~t[b];
       } else {
       for (int b = 0; b < s.N - 1; ++b) {
         if (b >= a) break;
@@ -1354,15 +1374,17 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // holds all robots; other lanes of other builds read robot 0)
   const int ag = (FRONT && FrontQuad<NSM>::ok) ? (C.sub & (N - 1)) : (C.sub < N ? C.sub : 0);
   // absent inputs read a harmless valid byte instead (no branch, no wait)
-  const uint8_t* ab = is_step ? actions + (size_t)e * N : reinterpret_cast<const uint8_t*>(s.pos);
+  const uint8_t* ab = is_step ? actions : reinterpret_cast<const uint8_t*>(s.pos);
+  const uint32_t eN = (uint32_t)e * (uint32_t)N;
   const uint8_t* mb = env_mask != nullptr ? env_mask + e : reinterpret_cast<const uint8_t*>(s.pos);
-  const int2 p0 = reinterpret_cast<const int2*>(s.pos)[(size_t)e * N + ag];
-  const int act_raw = ab[ag], act0_raw = ab[0], req_raw = mb[0];
-  const int g0 = s.env_grid[e];
-  const uint64_t moved0 = s.moved[e];
-  const uint32_t free_old = s.free_cnt[e], vis_old = s.vis_cnt[e];
-  const int currstep0 = s.currstep[e];
-  const double dthresh0 = s.done_thresh[e];
+  const int2 p0 = el<O32>(reinterpret_cast<const int2*>(s.pos), eN + ag);
+  const int act_raw = el<O32>(ab, is_step ? eN + ag : 0), act0_raw = el<O32>(ab, is_step ? eN : 0);
+  const int req_raw = mb[0];
+  const int g0 = el<O32>(s.env_grid, e);
+  const uint64_t moved0 = el<O32>(s.moved, e);
+  const uint32_t free_old = el<O32>(s.free_cnt, e), vis_old = el<O32>(s.vis_cnt, e);
+  const int currstep0 = el<O32>(s.currstep, e);
+  const double dthresh0 = el<O32>(s.done_thresh, e);
   const bool lidar = s.sensor == 0;
   const int nbl = lidar ? s.nbeams : 1;  // a square env reads a dummy record
   const int4 bm0 = reinterpret_cast<const int4*>(lidar ? (const void*)s.beams : (const void*)s.pos)
@@ -1392,6 +1414,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     L.sc->cnt_vis = 0;
     L.sc->do_reset = 0;
     L.sc->dist_hit = 0;
+    L.sc->zero = 0;
   }
   if (s.dist && C.sub < N) {  // dist_reward: M and witness of each free map
     const int2 mw = reinterpret_cast<const int2*>(s.dist_mw)[(size_t)e * N + C.sub];
@@ -1435,7 +1458,7 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #endif
     // count_nonzero(grid > 0) for percent_covered: kept in a register until
     // the reward (no wait here)
-    const int numfree = s.numfree[g0];
+    const int numfree = el<O32>(s.numfree, g0);
     __syncthreads();
     STAMP(2);
 #if defined(MC_ABL) && (MC_ABL == 10 || MC_ABL == 12)
@@ -1491,16 +1514,16 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       bool done = false;
       if (covered) { dt += s.dincr; done = true; }           // :540-543
       else if (cs == s.maxsteps) done = true;                // :544-545
-      reward_out[e] = r;
-      done_out[e] = done ? 1 : 0;
+      el<O32>(reward_out, e) = r;
+      el<O32>(done_out, e) = done ? 1 : 0;
       if (done) {  // the episode record (Utils/utils.py:138-141)
-        s.ep_pc[e] = exact1 ? (double)fc / (double)numfree : pc;
-        s.ep_len[e] = cs;
+        el<O32>(s.ep_pc, e) = exact1 ? (double)fc / (double)numfree : pc;
+        el<O32>(s.ep_len, e) = cs;
       }
-      s.free_cnt[e] = fc;
-      s.vis_cnt[e] = vc;
-      s.currstep[e] = cs;
-      s.done_thresh[e] = dt;
+      el<O32>(s.free_cnt, e) = fc;
+      el<O32>(s.vis_cnt, e) = vc;
+      el<O32>(s.currstep, e) = cs;
+      el<O32>(s.done_thresh, e) = dt;
       c->do_reset = (done && s.auto_reset) ? 1 : 0;
     }
     __syncthreads();
@@ -1536,8 +1559,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 
   if (active || reset_req || sent_reset) {
     if (C.sub < N)
-      reinterpret_cast<int2*>(s.pos)[(size_t)e * N + C.sub] = make_int2(L.x[C.sub], L.y[C.sub]);
-    if (C.sub == 0) s.moved[e] = L.sc->moved;
+      el<O32>(reinterpret_cast<int2*>(s.pos), (uint32_t)e * (uint32_t)N + C.sub) = make_int2(L.x[C.sub], L.y[C.sub]);
+    if (C.sub == 0) el<O32>(s.moved, e) = L.sc->moved;
     // dist_reward: a reset map, or one whose witness got closer than M,
     // has an unknown M now (recomputed by the full transform, mc_dist.hip)
     if (s.dist && C.sub < N &&

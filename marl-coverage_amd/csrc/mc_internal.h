@@ -48,6 +48,7 @@ static_assert(sizeof(Beam) == 16, "Beam is 16 bytes");
 //   grid_neg/grid_pos  u64 [G][MT]      tiles of grid < 0 / grid > 0
 //   freem/obstm        u64 [B][N][MT]   per-agent _free_pad/_obst_pad
 //   vis                u64 [B][MT]      _visited (union of free maps)
+// (each mask array has one more tile at its end that is always zero)
 // with MT = TRS * TCS * 16 tiles per map in tile_index order.
 //   pos                i32 [B][N][2]       (_xinds, _yinds)
 struct State {
