@@ -1482,7 +1482,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #endif
     __syncthreads();
     STAMP(5);
-    if (C.sub == 0) {
+    // every lane of the slot computes the reward and done (the same values:
+    // no broadcast round trip or barrier before the stores); lane 0 stores
+    bool do_reset;
+    {
       Scal* c = L.sc;
       const uint32_t fc = free_old + c->cnt_free;
       const uint32_t vc = vis_old + c->cnt_vis;
@@ -1514,21 +1517,26 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       bool done = false;
       if (covered) { dt += s.dincr; done = true; }           // :540-543
       else if (cs == s.maxsteps) done = true;                // :544-545
-      el<O32>(reward_out, e) = r;
-      el<O32>(done_out, e) = done ? 1 : 0;
-      if (done) {  // the episode record (Utils/utils.py:138-141)
-        el<O32>(s.ep_pc, e) = exact1 ? (double)fc / (double)numfree : pc;
-        el<O32>(s.ep_len, e) = cs;
+      do_reset = done && s.auto_reset;
+      if (C.sub == 0) {
+        el<O32>(reward_out, e) = r;
+        el<O32>(done_out, e) = done ? 1 : 0;
+        if (done) {  // the episode record (Utils/utils.py:138-141)
+          el<O32>(s.ep_pc, e) = exact1 ? (double)fc / (double)numfree : pc;
+          el<O32>(s.ep_len, e) = cs;
+        }
+        el<O32>(s.free_cnt, e) = fc;
+        el<O32>(s.vis_cnt, e) = vc;
+        el<O32>(s.currstep, e) = cs;
+        el<O32>(s.done_thresh, e) = dt;
+        c->do_reset = do_reset ? 1 : 0;
       }
-      el<O32>(s.free_cnt, e) = fc;
-      el<O32>(s.vis_cnt, e) = vc;
-      el<O32>(s.currstep, e) = cs;
-      el<O32>(s.done_thresh, e) = dt;
-      c->do_reset = (done && s.auto_reset) ? 1 : 0;
     }
-    __syncthreads();
+    // several waves: the slot's Scal reads above come before reset_env's
+    // writes (one wave: its LDS operations complete in order)
+    if constexpr (NT > 64) __syncthreads();
     STAMP(6);
-    if (!L.sc->do_reset) {
+    if (!do_reset) {
       store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
       STAMP(7);
     } else {
