@@ -249,9 +249,11 @@ def main():
     elapsed, kern_ms = timed_launches(lambda i, st: env.step_raw(actions[W + i].data_ptr(), rp, dp, op, st),
                                       dev, K, args.launch)
     env.check()
-    listed = None
+    listed = dj_listed = None
     if dr:  # maps the last step sent to the full distance transform (diagnostic)
         listed = int(env.get_state(marlcov._lib.FIELD_DIST_LISTED).item())
+    if dj:  # (env, agent) paths the last step sent to the full-map BFS (diagnostic)
+        dj_listed = int(env.get_state(marlcov._lib.FIELD_DJ_LISTED).item())
 
     # scalar episode-return statistics: the only collective (outside timing)
     reward_sum += env.reward
@@ -285,7 +287,8 @@ def main():
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
                    "launch": LAUNCH_DESC[args.launch],
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
-                   **({"dist_full_transforms_last_step": listed} if dr else {})},
+                   **({"dist_full_transforms_last_step": listed} if dr else {}),
+                   **({"dijkstra_full_map_paths_last_step": dj_listed} if dj else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),

@@ -134,7 +134,11 @@ enum {
      auto-reset clears the counters: the Utils/utils.py:141 statistic       */
   MC_FIELD_EP_PC = 16,       /* double [B] percent_covered() at the episode end */
   MC_FIELD_EP_LEN = 17,      /* int32  [B] _currstep at the episode end        */
-  MC_FIELD_COUNT = 18
+  /* dijkstra_input configs only (MC_EINVAL otherwise):                        */
+  MC_FIELD_DJ_LISTED = 18,   /* uint32 [1] (env, agent) paths the last step sent
+                                to the full-map BFS: nearest unexplored cell
+                                more than 24 steps away (read-only diagnostic) */
+  MC_FIELD_COUNT = 19
 };
 
 int32_t mc_abi_version(void);

@@ -21,7 +21,7 @@ ACT_NOOP = 4
 (FIELD_POS, FIELD_MOVED, FIELD_FREE, FIELD_OBST, FIELD_VISITED, FIELD_FREE_COUNT,
  FIELD_VISITED_COUNT, FIELD_CURRSTEP, FIELD_DONE_THRESH, FIELD_ENV_GRID, FIELD_EPISODE,
  FIELD_NUMFREE, FIELD_GRID_NEG, FIELD_GRID_POS, FIELD_DIST_MW, FIELD_DIST_LISTED, FIELD_EP_PC,
- FIELD_EP_LEN) = range(18)
+ FIELD_EP_LEN, FIELD_DJ_LISTED) = range(19)
 
 
 class McConfig(ctypes.Structure):

@@ -25,7 +25,7 @@ _FIELD_DTYPES = {
     _lib.FIELD_DONE_THRESH: "float64", _lib.FIELD_ENV_GRID: "int32", _lib.FIELD_EPISODE: "int32",
     _lib.FIELD_NUMFREE: "int32", _lib.FIELD_GRID_NEG: "int64", _lib.FIELD_GRID_POS: "int64",
     _lib.FIELD_DIST_MW: "int32", _lib.FIELD_DIST_LISTED: "int32",
-    _lib.FIELD_EP_PC: "float64", _lib.FIELD_EP_LEN: "int32",
+    _lib.FIELD_EP_PC: "float64", _lib.FIELD_EP_LEN: "int32", _lib.FIELD_DJ_LISTED: "int32",
 }
 
 
@@ -260,7 +260,7 @@ class BatchCoverageEnv:
             _lib.FIELD_ENV_GRID: (B,), _lib.FIELD_EPISODE: (B,), _lib.FIELD_NUMFREE: (G,),
             _lib.FIELD_GRID_NEG: (G,) + mw, _lib.FIELD_GRID_POS: (G,) + mw,
             _lib.FIELD_DIST_MW: (B, N, 2), _lib.FIELD_DIST_LISTED: (1,),
-            _lib.FIELD_EP_PC: (B,), _lib.FIELD_EP_LEN: (B,),
+            _lib.FIELD_EP_PC: (B,), _lib.FIELD_EP_LEN: (B,), _lib.FIELD_DJ_LISTED: (1,),
         }[field]
 
     def get_state(self, field):

@@ -24,7 +24,7 @@ hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stre
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
 hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* obs,
-                           hipStream_t stream);
+                           uint32_t* list, bool window, hipStream_t stream);
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream);
 hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
@@ -33,7 +33,8 @@ size_t dist_lds_bytes(const State& s, int pad);
 int dist_max_rows();
 size_t dijkstra_lds_bytes(const State& s, int pad);
 hipError_t launch_minimap(const State& s, int mini, double* out, hipStream_t stream);
-__global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out);
+__global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out,
+                                const uint32_t* list, uint32_t* count);
 }  // namespace mc
 
 namespace {
@@ -66,6 +67,8 @@ struct Env {
   int nt = 128;
   int epw = 1;  // envs per workgroup (2: two envs share one wave)
   size_t dj_lds = 0;  // dijkstra_input: LDS bytes of the BFS kernel
+  uint32_t* dj_list = nullptr;  // dijkstra_input: count, done, last count + [B*N] items (full-map BFS)
+  bool dj_window = true;        // dijkstra_input: window kernel first (MARLCOV_DJ_FULL=1: off)
   size_t dt_lds = 0;  // dist_reward: LDS bytes of the distance kernel
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
@@ -107,6 +110,7 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_DIST_LISTED: return {E->dist_list, E->dist_list ? 4 : -1};
     case MC_FIELD_EP_PC: return {s.ep_pc, B * 8};
     case MC_FIELD_EP_LEN: return {s.ep_len, B * 4};
+    case MC_FIELD_DJ_LISTED: return {E->dj_list ? E->dj_list + 2 : nullptr, E->dj_list ? 4 : -1};
     default: return {nullptr, -1};
   }
 }
@@ -334,6 +338,15 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
                   "device's %d B per workgroup", need, c.width, c.length, maxlds);
     }
     E->dj_lds = need;
+    void* lq = nullptr;
+    if (dev_alloc(E, &lq, ((size_t)s.B * s.N + 3) * 4) != MC_OK) {
+      std::string msg = g_err;
+      mc_destroy(E);
+      return fail(MC_EHIP, "dijkstra_input state: %s", msg.c_str());
+    }
+    E->dj_list = (uint32_t*)lq;
+    const char* fo = getenv("MARLCOV_DJ_FULL");  // parity tests: every item on the full map
+    E->dj_window = !(fo && atoi(fo) == 1);
   }
   if (c.dist_reward) {
     if (c.width + c.length + 4 * c.pad >= 65535) {
@@ -595,7 +608,8 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
   if (E->dj_lds > 65536)
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&mc::dijkstra_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)E->dj_lds));
-  HIP_TRY(mc::launch_dijkstra(E->s, E->cfg.pad, 3, E->s.Lc, (uint8_t*)dev_obs, st));
+  HIP_TRY(mc::launch_dijkstra(E->s, E->cfg.pad, 3, E->s.Lc, (uint8_t*)dev_obs, E->dj_list,
+                              E->dj_window, st));
   return MC_OK;
 }
 
@@ -681,7 +695,8 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   if (!E || !dev_src) return fail(MC_EINVAL, "mc_set_state: null argument");
   FieldDesc d = field(E, f);
   if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
-  if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED || f == MC_FIELD_EP_PC || f == MC_FIELD_EP_LEN)
+  if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED || f == MC_FIELD_EP_PC || f == MC_FIELD_EP_LEN ||
+      f == MC_FIELD_DJ_LISTED)
     return fail(MC_EINVAL, "field %d is derived state (read-only)", f);
   if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   HIP_TRY(hipSetDevice(E->device));

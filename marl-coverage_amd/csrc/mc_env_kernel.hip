@@ -1225,24 +1225,27 @@ __device__ __forceinline__ void write_obs(const State& s, const Ctx<NT, EPW, WT>
   }
 }
 
-// Compile-time obs shape (3 layers, E*E <= 28 bits, whole dwords per env):
-// lane j < 3N of a slot builds the E*E-bit crop of block j = (agent j / 3,
-// layer j % 3) -- layer 0 from the robot cells, layers 1 and 2 from one LDS
+// Compile-time obs shape (LC = 3 layers, or 4 with the dijkstra layer, which
+// is written here as zeros and then by mc_dijkstra.hip; E*E <= 28 bits, whole
+// dwords per env): lane j < LC*N of a slot builds the E*E-bit crop of block
+// j = (agent j / LC, layer j % LC) -- layer 0 from the robot cells, layers 1
+// and 2 from one LDS
 // byte per crop row and tile (the crop's bytes in the post-step tiles).  The
 // wave's envs are consecutive, so their obs are one run of dwords: lane l
 // writes dwords l, l + 64, ...; dword d is the nibble at bit 4d of the
 // slot's crop stream (fetched from the crop lanes by ds_bpermute), spread to
 // bytes by one multiply.  No per-row or per-layer branches.
-template <int EGO, int NS>
+template <int EGO, int NS, int LC = 3>
 struct ObsFast {
-  static constexpr int E = 2 * EGO + 1, EE = E * E, NB = 3 * NS;
-  static constexpr bool ok = EGO > 0 && NS > 0 && EE <= 28 && (NB * EE) % 4 == 0;
+  static constexpr int E = 2 * EGO + 1, EE = E * E, NB = LC * NS;
+  static constexpr bool ok = EGO > 0 && NS > 0 && EE <= 28 && (NB * EE) % 4 == 0 &&
+                             (LC == 3 || LC == 4);
 };
 
-template <int NT, int EPW, typename WT, int NS, int EGO>
+template <int NT, int EPW, typename WT, int NS, int EGO, int LC = 3>
 __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW, WT>& C,
                                                uint8_t* obs_out) {
-  using OF = ObsFast<EGO, NS>;
+  using OF = ObsFast<EGO, NS, LC>;
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   constexpr int E = OF::E, EE = OF::EE, NB = OF::NB;
   static_assert(NB <= LPE, "one crop per lane");
@@ -1250,8 +1253,8 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
   const int TW = s.TW;
   // ---- crops
   const int j = C.sub < NB ? C.sub : 0;
-  const int a = (j * 86) >> 8;  // j / 3 for j < 128
-  const int layer = j - 3 * a;
+  const int a = LC == 3 ? (j * 86) >> 8 : j >> 2;  // j / LC for j < 128
+  const int layer = j - LC * a;
   const int xa = L.x[a], ya = L.y[a];
   const uint64_t moved = L.sc->moved;
   uint32_t rp = 0;  // layer 0: robot_pad crop (robots that moved since the reset)
@@ -1274,7 +1277,7 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
     const uint32_t w = (uint32_t)p[0] | ((uint32_t)p[8] << 8);
     fo |= ((w >> (ly0 & 7)) & ((1u << E) - 1u)) << (r * E);
   }
-  const uint32_t crop = layer == 0 ? rp : fo;
+  const uint32_t crop = layer == 0 ? rp : (layer <= 2 ? fo : 0u);  // layer 3: dijkstra
   // ---- dwords of the wave's obs run
   constexpr int DPE = NB * EE / 4;       // dwords per env (a cell is one byte)
   constexpr int D = EPW * DPE;           // dwords per wave
@@ -1580,9 +1583,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
 #ifdef MC_OBS_SLOW
   if constexpr (false) {
 #else
-  if constexpr (ObsFast<SH::EGO, SH::N>::ok && NT == 64 && ObsFast<SH::EGO, SH::N>::NB <= CtxT::LPE) {
+  if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&
+                ObsFast<SH::EGO, SH::N, SH::LC>::NB <= CtxT::LPE) {
 #endif
-    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO>(s, C, obs_out);  // every lane of the wave
+    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the wave
   } else {
     if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
   }
@@ -1636,15 +1640,22 @@ hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const ui
   const uint64_t mtb = (uint64_t)s.MT * 8;
   const bool fits32 = (uint64_t)s.B * s.N * mtb < (1ull << 32) && (uint64_t)s.G * mtb < (1ull << 32);
   using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;    // the bench workload
+  using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs layers)
   using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;  // 360 beams, R=20
   using ShapeC5 = Shape<16, 10, 21, 0, 10, 8>;   // 16 agents, dist_reward (4 obs layers)
   if (epw == 2) {
     if (narrow && fits32 && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
+    else if (narrow && fits32 && getenv_spec() && ShapeC2D::matches(s))
+      MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2D);
     else if (narrow) MC_LAUNCH(64, 2, uint32_t);
     else MC_LAUNCH(64, 2, uint64_t);
   } else if (narrow) {
     if (nt == 64 && fits32 && getenv_spec() && ShapeC2::matches(s)) {
       MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2);
+      return hipGetLastError();
+    }
+    if (nt == 64 && fits32 && getenv_spec() && ShapeC2D::matches(s)) {
+      MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2D);
       return hipGetLastError();
     }
     if (nt == 128 && getenv_spec() && ShapeC5::matches(s)) {

@@ -166,13 +166,15 @@ __host__ __device__ inline size_t slot_stride(size_t slot_lds) {
 // (loop bounds, divisions and LDS offsets fold to constants and the march
 // unrolls); 0 leaves the field to the runtime State.  The launcher picks a
 // specialised instantiation only when the runtime State matches it exactly.
-template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0>
+// LC: obs layers of an EGO shape (3; 4 with dijkstra_input, whose layer 3 the
+// dijkstra kernel writes after the env kernel).
+template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3>
 struct Shape {
-  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_;
+  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_, LC = LC_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
            (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
-           (EGO_ == 0 || (s.ego == EGO_ && s.Lc == 3)) &&
+           (EGO_ == 0 || (s.ego == EGO_ && s.Lc == LC_ && !s.dist)) &&
            (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_)) &&
            (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_));
   }
@@ -196,13 +198,13 @@ __device__ __forceinline__ void specialize(State& s) {
   if constexpr (SH::EGO > 0) {
     s.ego = SH::EGO;
     s.E = 2 * SH::EGO + 1;
-    s.Lc = 3;
+    s.Lc = SH::LC;
     s.mg_E = magic_div(2 * SH::EGO + 1);
-    s.mg_LcE = magic_div(3 * (2 * SH::EGO + 1));
+    s.mg_LcE = magic_div(SH::LC * (2 * SH::EGO + 1));
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
   if constexpr (SH::KN > 0) s.beam_kmin = SH::KN;
-  if constexpr (SH::EGO > 0) s.dist = 0;  // EGO matches only Lc == 3: no dist layer
+  if constexpr (SH::EGO > 0) s.dist = 0;  // EGO shapes match only configs without dist_reward
 }
 
 }  // namespace mc

@@ -419,3 +419,69 @@ def test_batch_matches_oracle_full_beam_table(torch_cuda, name, monkeypatch):
     equivalent: mc_set_beam_table, State::beam_common)."""
     monkeypatch.setenv("MARLCOV_BEAM_TABLE", "1")
     test_batch_matches_oracle(torch_cuda, name)
+
+
+@pytest.mark.parametrize("full", [False, True], ids=["window", "full_map"])
+def test_dijkstra_far_targets(torch_cuda, monkeypatch, full):
+    """dijkstra_input with the nearest unexplored cell 1..300 steps away
+    (dijkstra.py:112-187): the window kernel's exact depth (24 layers) and its
+    edges, the full-map kernel for the items it lists, robots near the map
+    border, and fully explored maps (empty path: the pad ring walled off by
+    observed border obstacles).  MARLCOV_DJ_FULL=1 sends every item to the
+    full-map kernel."""
+    import marlcov
+    from marlcov import _lib
+    from marlcov.tiles import cells_to_tiles
+    torch = torch_cuda
+    if full:
+        monkeypatch.setenv("MARLCOV_DJ_FULL", "1")
+    else:
+        monkeypatch.delenv("MARLCOV_DJ_FULL", raising=False)
+    cfg = base_cfg(numrobot=3, dijkstra_input=1, sensor_config={"num_lasers": 9, "range": 3})
+    rs = np.random.RandomState(11)
+    B, N = 10, 3
+    grids = [bern(rs, 110, 96, 0.08) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False)
+    env.reset()
+    st = device_state(env)
+    W, L = env.width, env.length
+    X, Y = np.meshgrid(np.arange(W), np.arange(L), indexing="ij")
+    depths = [1, 6, 22, 23, 24, 25, 26, 31, 45, 80, 300]
+    free = np.zeros((B, N, W, L), np.uint8)
+    obst = np.zeros((B, N, W, L), np.uint8)
+    for b in range(B):
+        neg = st["neg"][st["env_grid"][b]][:W, :L]
+        for i in range(N):
+            D = depths[(b + 4 * i) % len(depths)]
+            x, y = st["pos"][b, i]
+            near = (np.abs(X - x) + np.abs(Y - y)) < D
+            free[b, i] = near & (neg == 0)
+            obst[b, i] = near & (neg == 1)
+    vis = free.max(axis=1)
+
+    def put(field, a):
+        env.set_state(field, torch.from_numpy(np.ascontiguousarray(a)))
+
+    put(_lib.FIELD_FREE, cells_to_tiles(free, blocks=True).view(np.int64))
+    put(_lib.FIELD_OBST, cells_to_tiles(obst, blocks=True).view(np.int64))
+    put(_lib.FIELD_VISITED, cells_to_tiles(vis, blocks=True).view(np.int64))
+    put(_lib.FIELD_FREE_COUNT, free.reshape(B, -1).sum(1).astype(np.int32))
+    put(_lib.FIELD_VISITED_COUNT, vis.reshape(B, -1).sum(1).astype(np.int32))
+    st = device_state(env)
+    refs = [oracle_from_device(st, b, cfg) for b in range(B)]
+    listed = 0
+    for t in range(4):
+        acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        listed = max(listed, int(env.get_state(_lib.FIELD_DJ_LISTED).item()))
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"far t={t} env {b}"
+            assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), tag
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+    if not full:
+        assert listed > 0  # some paths were farther than the window holds
+    env.check()
