@@ -191,6 +191,10 @@ def main():
                     help="stream: K back-to-back launches; graph: uploaded hipGraph replay; "
                          "events: per-launch HIP events")
     ap.add_argument("--eager", action="store_true", help="alias of --launch events")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (nccl = RCCL over xGMI).  gloo rehearses the "
+                         "multi-rank flow on fewer GPUs than ranks (ranks share the visible GPUs "
+                         "round-robin; the rate is then not a scaling number)")
     args = ap.parse_args()
     if args.eager:
         args.launch = "events"
@@ -213,10 +217,15 @@ def main():
     import marlcov
     from marlcov.shards import aggregate_rate, rank_seeds, reduce_run
 
+    if args.dist_backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     if c.get("env") == "super":
         return bench_super(args, c, B, cpu, world, rank, dev)
@@ -337,9 +346,16 @@ def timed_launches(step_fn, dev, K, launch):
         torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    evs = [ev0, ev1]
     if launch == "events":
         starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
         ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+        evs += starts + ends
+    # torch creates a HIP event at its first record: do that here, outside the
+    # timed region (an event created inside it costs ~tens of us of host time
+    # before the first launch)
+    for ev in evs:
+        ev.record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
