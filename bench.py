@@ -74,14 +74,19 @@ def sg_algorithmic_bytes_per_env_step(n_agents, r, W, L):
 def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3, full_map_cells=0):
     """per agent s^2 (int8 grid window) + 4*ceil(s^2/8) (free and
     obst bit windows, read+write) + 2*ceil(s^2/8) (union window read+write) +
-    obs bytes + 1 (action) + 8 (position r/w); per env 32 B.  Whole-map layers
-    (dijkstra_input; C5's distance map) add a read of the agent's free and obst
-    bit maps: 2*ceil(cells/8) per agent, as §8(d) prices C5."""
+    obs bytes + 1 (action) + 8 (position r/w); per env 32 B.  Map-wide layers
+    add a read of the agent's free and obst bit maps over `full_map_cells`
+    cells: 2*ceil(cells/8) per agent -- C5's distance map over the whole map,
+    as §8(d) prices it; dijkstra_input over the 64 x 64 BFS window its kernel
+    reads (the paths it lists for the full map are extra)."""
     s = 2 * math.ceil(beam_range) + 1
     bits = math.ceil(s * s / 8)
     obs = layers * (2 * ego + 1) ** 2
     full = 2 * math.ceil(full_map_cells / 8) if full_map_cells else 0
     return n_agents * (s * s + 6 * bits + obs + 1 + 8 + full) + 32
+
+
+DJ_WINDOW_CELLS = 64 * 64  # csrc/mc_dijkstra.hip: dijkstra_window_kernel
 
 
 # ---------------------------------------------------------------------------
@@ -277,7 +282,7 @@ def main():
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
                                          layers=3 + (4 if dr else 0) + (1 if dj else 0),
                                          full_map_cells=(c["width"] + 2 + 2 * cfg["egoradius"]) ** 2
-                                         if (dj or dr) else 0)
+                                         if dr else (DJ_WINDOW_CELLS if dj else 0))
     achieved = bpe * B / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
     line = {
@@ -300,8 +305,11 @@ def main():
                    **({"dijkstra_full_map_paths_last_step": dj_listed} if dj else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": traffic, "kernel": "mc::env_kernel", "kernel_us": round(kern_ms * 1e3, 3),
-                     "kernel_us_from": KERNEL_US_FROM[args.launch],
+                     "traffic": traffic,
+                     "kernel": "mc::env_kernel" + (" + mc::dijkstra_window_kernel + mc::dijkstra_kernel (one step)"
+                                                   if dj else " + the distance kernels (one step)" if dr else ""),
+                     "kernel_us": round(kern_ms * 1e3, 3),
+                     "kernel_us_from": KERNEL_US_FROM[args.launch] + (" (every kernel of a step)" if dj or dr else ""),
                      "alg_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }

@@ -112,6 +112,14 @@ BATCH_CASES = {
                           lambda rs: tri(rs, 36, 28), 8, 60),
     "dijkstra_c2_like": (base_cfg(numrobot=4, dijkstra_input=1), lambda rs: bern(rs, 128, 128, 0.1),
                          4, 12),
+    # the BFS window (64 x 64 around the robot's tile) against tiny and wide
+    # maps, a 12-cell pad ring (targets in the ring) and a 25-cell crop
+    "dijkstra_ego12_tiny": (base_cfg(numrobot=2, dijkstra_input=1, egoradius=12,
+                                     sensor_config={"num_lasers": 7, "range": 3}),
+                            lambda rs: bern(rs, 9, 7, 0.15), 6, 30),
+    "dijkstra_wide_40x150": (base_cfg(numrobot=3, dijkstra_input=1,
+                                      sensor_config={"num_lasers": 9, "range": 4}),
+                             lambda rs: tri(rs, 40, 150), 4, 40),
     # dist_reward: float32 distance terms in the reward and
     # the float obs layer; with dijkstra_input too the path overwrites it
     "dist_lidar_n3": (base_cfg(numrobot=3, dist_reward=1, sensor_config={"num_lasers": 15, "range": 5}),
