@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 4
+#define MARLCOV_ABI_VERSION 5
 
 enum {
   MC_OK = 0,
