@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kDjThreads) void dijkstra_kernel(State s, int pad, 
 }
 
 // ---- window kernel ---------------------------------------------------------
-constexpr int kDjWinDepth = 24;  // BFS layers the 64 x 64 window holds exactly
+constexpr int kDjWinDepth = 24;  // BFS layers the 64 x 64 window holds exactly (a multiple of 3)
 
 // whole-wave lane shifts of a 64-bit row (DPP wave_shr:1 / wave_shl:1; the
 // lane past the end reads 0): row r - 1 / row r + 1 of the window at lane r
@@ -314,9 +314,13 @@ __global__ __launch_bounds__(64) void dijkstra_window_kernel(State s, int pad, i
 
   // ---- BFS by layers in registers ---------------------------------------------
   // avail: cells not reached yet; m0 / m1: layers j = 1 / 2 (mod 3).  Three
-  // layers per trip (the mod-3 plane of each is static); a frontier that dies
-  // out is noticed at the trip's last layer (the layers after an empty one are
-  // empty, so no target is missed in between).
+  // layers per trip (each one's mod-3 plane is static) and one target test
+  // per trip: a trip with a hit then finds its first layer that has one.
+  // Layers past d* (at most two) join the planes too; that is harmless: a
+  // neighbour of a cost-j cell has cost j-1, j or j+1, so the walk back's
+  // mod-3 test only ever meets those.  A frontier that dies out ends the
+  // search at the trip's end (the layers after an empty one are empty).
+  // depth is a multiple of 3 (launch_dijkstra).
   int dstar = -1, er = rs, ec = cs;
   bool full = false;
   uint64_t cur = r == rs ? (1ull << cs) : 0ull;
@@ -324,37 +328,41 @@ __global__ __launch_bounds__(64) void dijkstra_window_kernel(State s, int pad, i
   if (lane_bit(tg, rs, cs)) {
     dstar = 0;  // the start cell itself is unexplored
   } else {
-    int j = 0;
-#define MC_DJ_LAYER(MARK, LAST)                                                          \
-  {                                                                                    \
-    if (++j > depth) {                                                                 \
-      full = true;                                                                     \
-      break;                                                                           \
-    }                                                                                  \
-    const uint64_t nf =                                                                \
-        (cur | (cur << 1) | (cur >> 1) | row_above(cur) | row_below(cur)) & avail;    \
-    avail ^= nf;                                                                       \
-    cur = nf;                                                                          \
-    MARK;                                                                              \
-    const uint64_t hit = nf & tg;                                                      \
-    const uint64_t hr = __ballot(hit != 0);                                            \
-    if (hr) { /* the (x, y)-smallest target of the layer: lowest row, then column */   \
-      er = __ffsll((unsigned long long)hr) - 1;                                        \
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hit, er); \
-      const uint32_t hi =                                                              \
-          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hit >> 32), er);         \
-      ec = lo ? __ffs(lo) - 1 : 32 + __ffs(hi) - 1;                                    \
-      dstar = j;                                                                       \
-      break;                                                                           \
-    }                                                                                  \
-    if (LAST && !__ballot(nf != 0)) break; /* no reachable unexplored cell */         \
-  }
-    for (;;) {
-      MC_DJ_LAYER(m0 |= nf, false)
-      MC_DJ_LAYER(m1 |= nf, false)
-      MC_DJ_LAYER((void)0, true)
+    for (int j = 0;; j += 3) {
+      if (j >= depth) {
+        full = true;
+        break;
+      }
+      uint64_t nf[3];
+      nf[0] = (cur | (cur << 1) | (cur >> 1) | row_above(cur) | row_below(cur)) & avail;
+      avail ^= nf[0];
+      m0 |= nf[0];
+      nf[1] = (nf[0] | (nf[0] << 1) | (nf[0] >> 1) | row_above(nf[0]) | row_below(nf[0])) & avail;
+      avail ^= nf[1];
+      m1 |= nf[1];
+      nf[2] = (nf[1] | (nf[1] << 1) | (nf[1] >> 1) | row_above(nf[1]) | row_below(nf[1])) & avail;
+      avail ^= nf[2];
+      cur = nf[2];
+      if (__ballot(((nf[0] | nf[1] | nf[2]) & tg) != 0)) {
+        // the first layer of the trip with a target; its (x, y)-smallest one:
+        // lowest row, then column
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const uint64_t hit = nf[q] & tg;
+          const uint64_t hr = __ballot(hit != 0);
+          if (hr) {
+            er = __ffsll((unsigned long long)hr) - 1;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hit, er);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hit >> 32), er);
+            ec = lo ? __ffs(lo) - 1 : 32 + __ffs(hi) - 1;
+            dstar = j + 1 + q;
+            break;
+          }
+        }
+        break;
+      }
+      if (!__ballot(cur != 0)) break;  // no reachable unexplored cell: empty path
     }
-#undef MC_DJ_LAYER
   }
   if (full) {  // farther than the window holds: the full kernel solves it
     if (r == 0) list[atomicAdd(count, 1u)] = ea;
@@ -363,38 +371,34 @@ __global__ __launch_bounds__(64) void dijkstra_window_kernel(State s, int pad, i
 
   // ---- walk back (dijkstra.py:166-185): from each cell the first neighbour in
   // the order +x, -x, +y, -y whose cost is one less.  The choice of every
-  // reached cell at once, as two direction planes q = 2 d1 + d0; then the walk
-  // reads one bit pair per step.
-  uint64_t path = 0;
+  // reached cell at once, as two direction planes q = 2 d1 + d0 (a reached
+  // cell of cost >= 1 always has such a neighbour: its BFS parent); then the
+  // walk reads one bit pair per step (readlane, scalar).  Only crop cells are
+  // recorded: lane k keeps crop row k.
+  const int E = s.E, ego = s.ego;
+  const int cr0 = rs - ego, cc0 = cs - ego;  // crop origin (window coordinates)
+  uint32_t crop = 0;
   if (dstar >= 0) {
     const uint64_t k1 = m0, k2 = m1, k0 = ~ob & valid & ~avail & ~m0 & ~m1;  // reached, cost = 0 mod 3
     const uint64_t px_ = pred(k0, k1, k2, row_below(k0), row_below(k1), row_below(k2));
     const uint64_t mx_ = pred(k0, k1, k2, row_above(k0), row_above(k1), row_above(k2));
     const uint64_t py_ = pred(k0, k1, k2, k0 >> 1, k1 >> 1, k2 >> 1);
-    const uint64_t my_ = pred(k0, k1, k2, k0 << 1, k1 << 1, k2 << 1);
     const uint64_t d1 = ~px_ & ~mx_;
     const uint64_t d0 = (~px_ & mx_) | (d1 & ~py_);
-    const uint64_t any = px_ | mx_ | py_ | my_;
     int cu = er, cv = ec;
-    for (int j = dstar; j > 0; --j) {
-      path |= r == cu ? (1ull << cv) : 0ull;
-      if (!lane_bit(any, cu, cv)) {  // cannot happen: a cost-j cell has a cost-(j-1) neighbour
-        if (r == 0) atomicOr(s.err, ERR_WINDOW);
-        break;
-      }
+    for (int j = dstar;; --j) {
+      const int kr = cu - cr0, kc = cv - cc0;
+      if ((unsigned)kr < (unsigned)E && (unsigned)kc < (unsigned)E && r == kr) crop |= 1u << kc;
+      if (j == 0) break;
       const int q = (int)(2 * lane_bit(d1, cu, cv) + lane_bit(d0, cu, cv));
       cu += q == 0 ? 1 : (q == 1 ? -1 : 0);
       cv += q == 2 ? 1 : (q == 3 ? -1 : 0);
     }
-    path |= r == cu ? (1ull << cv) : 0ull;  // the start cell
   }
-  // ---- obs layer `layer`: crop row k = window row rs - ego + k, columns from cs - ego
-  const int E = s.E, ego = s.ego;
-  const int k = r - (rs - ego);
-  if ((unsigned)k < (unsigned)E) {
-    const uint32_t row = (uint32_t)(path >> (cs - ego));
-    uint8_t* dst = obs_out + ((size_t)ea * Lc + layer) * E * E + (size_t)k * E;
-    for (int c = 0; c < E; ++c) dst[c] = (uint8_t)((row >> c) & 1u);
+  // ---- obs layer `layer`: crop row k = window row rs - ego + k ------------------
+  if (r < E) {
+    uint8_t* dst = obs_out + ((size_t)ea * Lc + layer) * E * E + (size_t)r * E;
+    for (int c = 0; c < E; ++c) dst[c] = (uint8_t)((crop >> c) & 1u);
   }
 }
 
@@ -419,7 +423,7 @@ hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* 
   static const int depth = [] {  // MARLCOV_DJ_DEPTH: fewer exact layers (diagnostics, A/B)
     const char* v = getenv("MARLCOV_DJ_DEPTH");
     const int d = v ? atoi(v) : kDjWinDepth;
-    return d >= 0 && d < kDjWinDepth ? d : kDjWinDepth;
+    return d >= 0 && d < kDjWinDepth ? d - d % 3 : kDjWinDepth;  // whole trips of 3 layers
   }();
   hipLaunchKernelGGL(dijkstra_window_kernel, dim3(items), dim3(64), 0, stream, s, pad, layer, Lc,
                      obs, list + 3, list, depth);
