@@ -153,7 +153,10 @@ template <int NT, int EPW, typename WT>
 struct Ctx {
   static constexpr int LPE = NT / EPW;            // lanes per env
   static constexpr int KI = kMaxItemsPerLane;     // staged tiles per lane
-  static constexpr int RPL = EPW == 1 ? 2 : 3;    // beams per lane per pass (C4 A/B: 4 or 6 are slower)
+#ifndef MC_RPL1
+#define MC_RPL1 2
+#endif
+  static constexpr int RPL = EPW == 1 ? MC_RPL1 : 3;  // beams per lane per pass (C4 A/B: 3, 4 or 6 are slower)
   int sub;    // lane within the env
   int lane0;  // first lane of this env's slot within the wave
   int e;      // env index
