@@ -185,6 +185,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
+    ap.add_argument("--global-envs", type=int, default=None,
+                    help="split this fixed global batch over the ranks (strong scaling, shard_range) "
+                         "instead of --envs per GPU (weak scaling)")
     # the GPU box's host share is 16 CPUs per GPU (os.cpu_count() there shows
     # the whole machine): one single-env oracle process per core
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -208,7 +211,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     c = CONFIGS[args.config]
-    B = args.envs or c["envs"]
+    # this rank's slice [e0, e1) of the global env batch; every device random
+    # stream is keyed by the global env id (marlcov.shards), so env e runs the
+    # same trajectory whatever the number of GPUs
+    from marlcov.shards import shard_range, weak_range
+    if args.global_envs:
+        e0, e1 = shard_range(args.global_envs, world, rank)
+        scaling = "strong"
+    else:
+        e0, e1 = weak_range(args.envs or c["envs"], rank)
+        scaling = "weak"
+    B = e1 - e0
+    total_envs = args.global_envs or B * world
     if args.maxsteps is None:
         args.maxsteps = c.get("maxsteps", 1000)
 
@@ -220,7 +234,7 @@ def main():
     import torch.distributed as dist
 
     import marlcov
-    from marlcov.shards import aggregate_rate, rank_seeds, reduce_run
+    from marlcov.shards import aggregate_rate, reduce_run, shard_seeds
 
     if args.dist_backend == "gloo":
         local %= max(1, torch.cuda.device_count())
@@ -232,22 +246,26 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    run = dict(e0=e0, total_envs=total_envs, scaling=scaling,
+               rehearsal=world > 1 and args.dist_backend == "gloo")
     if c.get("env") == "super":
-        return bench_super(args, c, B, cpu, world, rank, dev)
+        return bench_super(args, c, B, cpu, world, rank, dev, run)
     cfg = dict(BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
                maxsteps=args.maxsteps, **c.get("extra", {}))
     dj = bool(cfg.get("dijkstra_input"))
     dr = bool(cfg.get("dist_reward"))
     N = c["numrobot"]
-    seeds = rank_seeds(rank)
+    seeds = shard_seeds(e0)
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
                                                     seed=seeds["grid_seed"], num_grids=B),
-                                   device=dev, seed=seeds["env_seed"], auto_reset=True)
+                                   device=dev, seed=seeds["env_seed"], auto_reset=True,
+                                   env_offset=seeds["env_offset"])
     env.reset()
     K, W = args.steps, args.warmup
-    g = torch.Generator(device=dev)
-    g.manual_seed(seeds["action_seed"])
-    actions = torch.randint(0, 4, (W + K, B, N), dtype=torch.uint8, device=dev, generator=g)
+    # per-step actions keyed by (global env id, step), staged in HBM before timing
+    actions = torch.empty((W + K, B, N), dtype=torch.uint8, device=dev)
+    for i in range(W + K):
+        env.random_actions(seeds["action_seed"], i, out=actions[i])
     reward_sum = torch.zeros(B, dtype=torch.float64, device=dev)
     episodes = torch.zeros(B, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -276,7 +294,7 @@ def main():
     stats, elapsed = reduce_run(stats, elapsed, world)
 
     n_gpus = world
-    value = aggregate_rate(B, n_gpus, K, elapsed)
+    value = aggregate_rate(total_envs, K, elapsed)
     # §8(d): C5's float32 distance layer is 4 B per cell (100 B per agent at
     # E=5) and its two transforms read the whole bit map
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
@@ -294,12 +312,14 @@ def main():
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": None if run["rehearsal"] else run["scaling"],
         "vs_baseline": None,
         "dtype": "f64+u64",
-        "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
-        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * n_gpus,
-                   "launch": LAUNCH_DESC[args.launch],
+        "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions; Philox keyed by "
+                "global env id)",
+        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": total_envs,
+                   "launch": LAUNCH_DESC[args.launch], "kernel_variant": env.kernel_variant(),
+                   **dist_desc(args, world),
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
                    **({"dist_full_transforms_last_step": listed} if dr else {}),
                    **({"dijkstra_full_map_paths_last_step": dj_listed} if dj else {})},
@@ -317,6 +337,21 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dist_desc(args, world):
+    """Process-group facts for the config: the backend and the GPUs the ranks
+    really ran on (a gloo rehearsal shares fewer GPUs between its ranks: its
+    rate is not a scaling number, and the line says so)."""
+    import torch
+    if world == 1:
+        return {}
+    phys = torch.cuda.device_count()
+    d = {"dist_backend": "rccl" if args.dist_backend == "nccl" else "gloo", "physical_gpus": min(world, phys)}
+    if args.dist_backend == "gloo":
+        d["rehearsal"] = (f"{world} ranks over {min(world, phys)} visible GPU(s), gloo process group: "
+                          "multi-rank flow check, not a scaling measurement")
+    return d
 
 
 def timed_launches(step_fn, dev, K, launch):
@@ -399,25 +434,26 @@ LAUNCH_DESC = {"stream": "back-to-back stream launches", "graph": "hipGraph repl
                "events": "stream launches with per-launch events"}
 
 
-def bench_super(args, c, B, cpu, world, rank, dev):
+def bench_super(args, c, B, cpu, world, rank, dev, run):
     """SuperGridRL workload: one step = sg_step_kernel +
     sg_dist_kernel over every env of this GPU's shard."""
     import torch
     import torch.distributed as dist
 
     import marlcov
-    from marlcov.shards import aggregate_rate, rank_seeds, reduce_run
+    from marlcov.shards import aggregate_rate, reduce_run, shard_seeds
 
     N, W = c["numrobot"], c["width"]
     cfg = dict(SG_BASE, numrobot=N, **c["sg"])
-    seeds = rank_seeds(rank)
+    seeds = shard_seeds(run["e0"])
     env = marlcov.BatchSuperGridEnv(cfg, B, gen=dict(width=W, length=W, prob_obst=0.1, seed=seeds["grid_seed"],
                                                      num_grids=B),
-                                    device=dev, seed=seeds["env_seed"], auto_reset=True, maxsteps=args.maxsteps)
+                                    device=dev, seed=seeds["env_seed"], auto_reset=True, maxsteps=args.maxsteps,
+                                    env_offset=seeds["env_offset"])
     env.reset()
     K, Wm = args.steps, args.warmup
     g = torch.Generator(device=dev)
-    g.manual_seed(seeds["action_seed"])
+    g.manual_seed(seeds["action_seed"] + run["e0"])
     actions = torch.randint(0, 4, (Wm + K, B, N), dtype=torch.uint8, device=dev, generator=g)
     rp, dp = env.reward.data_ptr(), env.done.data_ptr()
     sp = torch.cuda.current_stream(dev).cuda_stream
@@ -430,7 +466,7 @@ def bench_super(args, c, B, cpu, world, rank, dev):
     env.check()
     stats = torch.stack([env.reward.sum(), env.done.to(torch.float64).sum()])
     stats, elapsed = reduce_run(stats, elapsed, world)
-    value = aggregate_rate(B, world, K, elapsed)
+    value = aggregate_rate(run["total_envs"], K, elapsed)
     bpe = sg_algorithmic_bytes_per_env_step(N, cfg["senseradius"], W, W)
     full_dist = os.environ.get("MARLCOV_SG_FULL_DIST") == "1"
     traffic = None if full_dist else load_traffic(args.config)
@@ -447,11 +483,13 @@ def bench_super(args, c, B, cpu, world, rank, dev):
         "metric": "env-steps/sec (whole node), SuperGridRL 4-agent 128x128 (SURVEY 8(f) rank 2; not the "
                   "BASELINE metric)",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": Wm,
-        "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True,
+        "scaling": None if run["rehearsal"] else run["scaling"],
         "vs_baseline": None, "dtype": "f64+u64+f32",
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
-        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": B * world,
-                   "launch": LAUNCH_DESC[args.launch], "parallelism": f"env-shard x{world}",
+        "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": run["total_envs"],
+                   "launch": LAUNCH_DESC[args.launch], **dist_desc(args, world),
+                   "parallelism": f"env-shard x{world}",
                    "auto_reset": True, "maxsteps": args.maxsteps},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "achieved_from": achieved_from,

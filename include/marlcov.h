@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 5
+#define MARLCOV_ABI_VERSION 6
 
 enum {
   MC_OK = 0,
@@ -91,6 +91,13 @@ typedef struct mc_config {
   int32_t mini_map_rad;       /* 'mini_map_rad' (> 0: float64 minimap layers
                                  3-4 via mc_set_minimap_obs; pad >= it)       */
   uint64_t seed;              /* batch extra: device Philox seed              */
+  /* Global ids (batch extras): env e of this handle is global env
+   * env_offset + e and pool grid g is global grid grid_offset + g.  Every
+   * device random stream (start-cell draws, the grid pick, mc_generate_grids,
+   * mc_random_actions) is keyed by the global id, so a shard of a global batch
+   * reproduces those envs bit for bit whatever the number of GPUs.          */
+  uint32_t env_offset;
+  uint32_t grid_offset;
 } mc_config;
 
 /* Derived geometry (mc_query). */
@@ -128,14 +135,14 @@ enum {
                                 L1 distance transform (-1 = unknown: the next
                                 POST runs the full transform), witness = a cell
                                 with d == M, (x << 16) | (y & 0xFFFF), map coords */
-  MC_FIELD_DIST_LISTED = 15, /* uint32 [1] maps the last POST sent to the full
+  MC_FIELD_DIST_LISTED = 15, /* int32 [1] maps the last POST sent to the full
                                 transform (read-only diagnostic)               */
   /* episode record (read-only), written when an env reports done, before an
      auto-reset clears the counters: the Utils/utils.py:141 statistic       */
   MC_FIELD_EP_PC = 16,       /* double [B] percent_covered() at the episode end */
   MC_FIELD_EP_LEN = 17,      /* int32  [B] _currstep at the episode end        */
   /* dijkstra_input configs only (MC_EINVAL otherwise):                        */
-  MC_FIELD_DJ_LISTED = 18,   /* uint32 [1] (env, agent) paths the last step sent
+  MC_FIELD_DJ_LISTED = 18,   /* int32 [1] (env, agent) paths the last step sent
                                 to the full-map BFS: nearest unexplored cell
                                 more than 24 steps away (read-only diagnostic) */
   MC_FIELD_COUNT = 19
@@ -165,9 +172,21 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams);
 int mc_set_grids(void* env, const int8_t* dev_grids, int32_t num_grids, void* stream);
 
 /* Synthetic pool: grid g interior cells are obstacles with probability
- * p_obst (Philox(seed, g)), border -1.  Same distribution as gridgen
+ * p_obst (Philox(seed, grid_offset + g)), border -1.  Same distribution as gridgen
  * (Utils/gridmaker.py:127-128); not the same bits. */
 int mc_generate_grids(void* env, uint64_t seed, double p_obst, void* stream);
+
+/* Synthetic per-agent action bytes for step `step`: dev_actions uint8 [B][N]
+ * uniform in {0..3} from Philox(seed, global env id, step) (SURVEY 8(d)
+ * "Actions (GPU)"), so a shard draws exactly the actions its envs draw in one
+ * big batch. */
+int mc_random_actions(void* env, uint64_t seed, int32_t step, uint8_t* dev_actions, void* stream);
+
+/* Name of the env-kernel instantiation the next mc_step / mc_reset launches
+ * (compiled shape or the generic kernel, lanes per workgroup, envs per
+ * workgroup), e.g. "env_kernel<64,2,u32,C2>".  Diagnostic: lets tests show
+ * which specialisation they cover.  The string is static. */
+const char* mc_kernel_variant(void* env);
 
 /* Which pool grid each env uses (int32 [B], device). */
 int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream);
@@ -250,6 +269,8 @@ typedef struct mc_sg_config {
   int32_t reset_grid_mode;    /* 0: keep the env's grid; 1: draw from the pool */
   int32_t pad_;
   uint64_t seed;              /* batch extra: device Philox seed              */
+  uint32_t env_offset;        /* global id of env 0 (see mc_config)           */
+  uint32_t grid_offset;       /* global id of pool grid 0                     */
 } mc_sg_config;
 
 typedef struct mc_sg_layout {

@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
@@ -53,6 +53,8 @@ class McConfig(ctypes.Structure):
         ("reset_grid_mode", ctypes.c_int32),
         ("mini_map_rad", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("env_offset", ctypes.c_uint32),
+        ("grid_offset", ctypes.c_uint32),
     ]
 
 
@@ -94,6 +96,8 @@ class McSgConfig(ctypes.Structure):
         ("reset_grid_mode", ctypes.c_int32),
         ("pad_", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("env_offset", ctypes.c_uint32),
+        ("grid_offset", ctypes.c_uint32),
     ]
 
 
@@ -127,6 +131,8 @@ SIGNATURES = [
     ("mc_set_grids", ctypes.c_int, [_VP, _VP, _I32, _VP]),
     ("mc_generate_grids", ctypes.c_int, [_VP, _U64, _D, _VP]),
     ("mc_set_env_grids", ctypes.c_int, [_VP, _VP, _VP]),
+    ("mc_random_actions", ctypes.c_int, [_VP, _U64, _I32, _VP, _VP]),
+    ("mc_kernel_variant", ctypes.c_char_p, [_VP]),
     ("mc_reset", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("mc_step", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("mc_field_bytes", _I64, [_VP, _I32]),

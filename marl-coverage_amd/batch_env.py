@@ -61,11 +61,16 @@ class BatchCoverageEnv:
     ``step`` / ``reset`` return the env's persistent output tensors (obs uint8
     [B, N, Lc, E, E], reward float64 [B], done uint8 [B]); they are
     overwritten by the next call — clone them to keep them.
+
+    ``env_offset`` / ``grid_offset`` (default: ``env_offset``) are the global
+    ids of env 0 and pool grid 0 when this handle is one shard of a larger
+    batch: every device random stream is keyed by global id, so
+    the shard's envs match the same envs of the whole batch bit for bit.
     """
 
     def __init__(self, env_config, num_envs, grids=None, *, gen=None, device="cuda",
                  seed=0, auto_reset=True, reset_grid_mode="keep", env_grid=None,
-                 sensor=None, want_adjacency=None):
+                 sensor=None, want_adjacency=None, env_offset=0, grid_offset=None):
         import torch
 
         self._torch = torch
@@ -125,6 +130,9 @@ class BatchCoverageEnv:
         c.auto_reset = int(bool(auto_reset))
         c.reset_grid_mode = {"keep": 0, "random": 1}[reset_grid_mode]
         c.seed = int(seed) & (2 ** 64 - 1)
+        c.env_offset = int(env_offset)
+        c.grid_offset = int(env_offset if grid_offset is None else grid_offset)
+        self.env_offset = c.env_offset
         self._cfg = c
 
         handle = ctypes.c_void_p()
@@ -182,9 +190,9 @@ class BatchCoverageEnv:
         if not getattr(self, "_h", None):  # closed
             return
         tab = np.ascontiguousarray(sensor.table(), dtype=np.float64)
-        self._cfg.num_beams = tab.shape[0]
         _lib.check(self.lib.mc_set_beam_table(self._h, tab.ctypes.data, tab.shape[0]),
                    "mc_set_beam_table")
+        self._cfg.num_beams = tab.shape[0]  # only once the device holds the table
 
     def _adj_ptr(self):
         return None if self.adj is None else self.adj.data_ptr()
@@ -244,6 +252,21 @@ class BatchCoverageEnv:
         if self.adj is not None:
             return (self.obs, self.adj), self.reward, self.done
         return self.obs, self.reward, self.done
+
+    def random_actions(self, seed, step, out=None):
+        """uint8 [B, N] actions uniform in {0..3} from Philox(seed, global env
+        id, step) (mc_random_actions): the same bytes for an env whatever the
+        shard it is stepped in."""
+        torch = self._torch
+        if out is None:
+            out = torch.empty((self.num_envs, self.num_agents), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.mc_random_actions(self._h, int(seed) & (2 ** 64 - 1), int(step), out.data_ptr(),
+                                              self._stream()), "mc_random_actions")
+        return out
+
+    def kernel_variant(self) -> str:
+        """The env-kernel instantiation mc_step launches (mc_kernel_variant)."""
+        return self.lib.mc_kernel_variant(self._h).decode()
 
     def step_raw(self, actions_ptr: int, reward_ptr: int, done_ptr: int, obs_ptr: int, stream: int):
         """Zero-overhead launch for benchmarks: raw device pointers / stream."""

@@ -23,6 +23,8 @@ int env_pack(const State& s);
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream);
 hipError_t launch_pack(const State& s, const int8_t* grids, hipStream_t stream);
 hipError_t launch_gen(const State& s, uint64_t seed, double p, hipStream_t stream);
+hipError_t launch_random_actions(const State& s, uint64_t seed, int step, uint8_t* out, hipStream_t stream);
+const char* env_variant(const State& s, int nt, int epw);
 hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* obs,
                            uint32_t* list, bool window, hipStream_t stream);
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
@@ -264,6 +266,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.auto_reset = c.auto_reset ? 1 : 0;
   s.grid_mode = c.reset_grid_mode;
   s.seed = c.seed;
+  s.env0 = c.env_offset;
+  s.grid0 = c.grid_offset;
 
   hipError_t he = hipSetDevice(hip_device);
   if (he != hipSuccess) {
@@ -586,6 +590,23 @@ int mc_generate_grids(void* env, uint64_t seed, double p_obst, void* stream) {
   HIP_TRY(hipMemsetAsync((void*)E->s.numfree, 0, (size_t)E->s.G * 4, st));
   HIP_TRY(mc::launch_gen(E->s, seed, p_obst, st));
   return check_numfree(E, st);
+}
+
+int mc_random_actions(void* env, uint64_t seed, int32_t step, uint8_t* dev_actions, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_actions) return fail(MC_EINVAL, "mc_random_actions: null argument");
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(mc::launch_random_actions(E->s, seed, step, dev_actions, (hipStream_t)stream));
+  return MC_OK;
+}
+
+const char* mc_kernel_variant(void* env) {
+  Env* E = as_env(env);
+  if (!E) {
+    fail(MC_EINVAL, "mc_kernel_variant: null env");
+    return "";
+  }
+  return mc::env_variant(E->s, E->nt, launch_epw(E));
 }
 
 int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {

@@ -37,20 +37,7 @@
 
 namespace mc {
 
-#ifdef MC_STAMPS
-#define STAMP(k)                                                                          \
-  do {                                                                                    \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    uint64_t _t;                                                                          \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
-    if (threadIdx.x == 0 && s.stamps) s.stamps[(size_t)blockIdx.x * EPW * 16 + (k)] = _t; \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-  } while (0)
-#else
-#define STAMP(k) \
-  do {           \
-  } while (0)
-#endif
+#include "mc_diag.h"  // STAMP(k): phase stamps of -DMC_STAMPS diagnostic builds
 
 // n / d via the magic reciprocal of mc_internal.h (magic == 0 encodes d == 1)
 __device__ __forceinline__ int udiv(int n, uint32_t magic) {
@@ -153,10 +140,7 @@ template <int NT, int EPW, typename WT>
 struct Ctx {
   static constexpr int LPE = NT / EPW;            // lanes per env
   static constexpr int KI = kMaxItemsPerLane;     // staged tiles per lane
-#ifndef MC_RPL1
-#define MC_RPL1 2
-#endif
-  static constexpr int RPL = EPW == 1 ? MC_RPL1 : 3;  // beams per lane per pass (C4 A/B: 3, 4 or 6 are slower)
+  static constexpr int RPL = EPW == 1 ? 2 : 3;  // beams per lane per pass (C4 A/B: 3, 4 or 6 are slower)
   int sub;    // lane within the env
   int lane0;  // first lane of this env's slot within the wave
   int e;      // env index
@@ -423,12 +407,8 @@ __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW,
       // 8*ti .. 8*ti+7 of the agent's block)
       const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
-#if defined(MC_ABL) && MC_ABL == 13
-      // timing ablation: no row-plane scatter (the march sees an empty grid)
-#else
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
-#endif
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
         const uint64_t ft = (I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
 #pragma unroll
@@ -728,11 +708,7 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
   // exec-masked OR on the single mark plane gains nothing either: 9.32 vs
   // 9.15 us.)
   const int delta = (int)(L.fpr - L.negr) * (int)sizeof(WT);
-#if defined(MC_ABL) && MC_ABL == 1
-  const uint32_t a = sink_m;  // timing ablation: no marks
-#else
   const uint32_t a = (on && !dup && !premarked) ? (R.P >> 6) : sink_m;
-#endif
   WT* tgt = reinterpret_cast<WT*>((char*)((lds_char*)(uintptr_t)a + delta));  // free or obstacle: the grid tells
   if (frow_valid) {  // dense: most rays skip; an exec-masked OR of the few that mark
     if (on && !dup && !premarked) lds_or<WT>(tgt, bit);
@@ -929,11 +905,7 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       cf += __popcll(I.nf[k]);
       uint64_t cand = fp & ~u0;
       const int a = I.a[k], gi = I.gi[k], gj = I.gj[k];
-#if defined(MC_ABL) && MC_ABL == 4
-      if constexpr (false) {  // timing ablation: no dedup
-#else
       if constexpr (NS > 0) {
-#endif
         // marks of lower-index agents in this tile: every read issued
         // unconditionally (own tile when unused), no loop-carried branch
         // (an agent whose block misses the tile, or b >= a, reads the
@@ -1010,9 +982,7 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
-#if !(defined(MC_ABL) && MC_ABL == 3)
   sense<NT, EPW, WT, SUK, KN>(s, C);
-#endif
   __syncthreads();
   STAMP(13);
   if (s.sensor == 0) {
@@ -1054,7 +1024,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
     s.episode[e] = ep;
     L.sc->ep = ep;
     if (s.grid_mode == 1) {
-      const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, (uint32_t)e, ep, 0x67726964u));
+      const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, s.env0 + (uint32_t)e, ep, 0x67726964u));
       const int g = (int)bounded(r.x, (uint32_t)s.G);
       L.sc->grid = g;
       s.env_grid[e] = g;
@@ -1093,7 +1063,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
     int px = INT32_MIN / 2, py = INT32_MIN / 2, placed = 0;
     for (int round = 0; round < 1024 && placed < N; ++round) {
       const uint32_t k = (uint32_t)(round * CPR + lane);
-      const uint4 r = philox(s.seed, make_uint4(k, (uint32_t)e, ep, 0x706c6163u));
+      const uint4 r = philox(s.seed, make_uint4(k, s.env0 + (uint32_t)e, ep, 0x706c6163u));
       const int cx = (int)bounded(r.x, (uint32_t)s.Wp);
       const int cy = (int)bounded(r.y, (uint32_t)s.Lp);
       uint64_t okm = slot_ballot(C, !grid_blocked(s, g, cx, cy));
@@ -1348,12 +1318,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   // (launch_env checks; the C5 shape's maps pass 4 GB)
   constexpr bool O32 = SH::N > 0 && SH::N <= 8;
   // register front (front_regs / moves_front): compiled agent count <= 8,
-  // one wave per workgroup; MC_NO_FRONT builds the LDS front (A/B)
-#ifdef MC_NO_FRONT
-  constexpr bool FRONT = false;
-#else
+  // one wave per workgroup
   constexpr bool FRONT = NSM > 0 && NT == 64;
-#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1436,13 +1402,6 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
   if (active) {
     STAMP(1);
     Items<KI> I;
-#if defined(MC_ABL) && MC_ABL == 12
-    // timing ablation: no second round trip (positions and scalars only)
-#pragma unroll
-    for (int k = 0; k < KI; ++k) { I.in[k] = false; I.a[k] = I.gi[k] = I.gj[k] = 0; }
-#elif defined(MC_ABL) && MC_ABL == 6
-    stage<NT, EPW, WT, KI, O32>(s, C, g0, false, I);  // timing ablation: grid tiles only
-#else
     if constexpr (FRONT) {
       // ---- round trip 2, issue: the robots' target-cell grid tiles first
       // (the moves wait only for them), then every staged tile; block
@@ -1461,20 +1420,11 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     } else {
       stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
     }
-#endif
     // count_nonzero(grid > 0) for percent_covered: kept in a register until
     // the reward (no wait here)
     const int numfree = el<O32>(s.numfree, g0);
     __syncthreads();
     STAMP(2);
-#if defined(MC_ABL) && (MC_ABL == 10 || MC_ABL == 12)
-    // timing ablation: the memory floor (no moves, sensing, merge or obs)
-#pragma unroll
-    for (int k = 0; k < KI; ++k) I.nf[k] = I.no[k] = I.nu[k] = 0;
-#else
-#if defined(MC_ABL) && MC_ABL == 7
-    // timing ablation: no moves
-#else
     // (the same loop on the scalar unit, robots read by v_readlane, was
     // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
     if constexpr (!FRONT) {  // (FRONT: moved during round trip 2)
@@ -1482,10 +1432,8 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
       __syncthreads();
     }
-#endif
     STAMP(3);
     sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN>(s, C, I);
-#endif
     __syncthreads();
     STAMP(5);
     // every lane of the slot computes the reward and done (the same values:
@@ -1514,8 +1462,10 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       // pc = count/numfree (:552), correctly rounded; thr <= pc.  With thr
       // == 1 (the default) the test is fc >= numfree exactly (counts are
       // < 2^24: a quotient below 1 rounds below 1), so the float64 divide
-      // runs only when the threshold or the episode record needs it
-      const bool exact1 = thr == 1.0;
+      // runs only when the threshold or the episode record needs it.  A
+      // grid with no cell > 0 takes the division: 0/0 = NaN is never covered,
+      // as in the reference
+      const bool exact1 = thr == 1.0 && numfree > 0;
       double pc = 0.0;
       if (!exact1) pc = (double)fc / (double)numfree;
       const bool covered = exact1 ? fc >= (uint32_t)numfree : thr <= pc;
@@ -1582,18 +1532,12 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
   }
   STAMP(8);
-#if !(defined(MC_ABL) && (MC_ABL == 5 || MC_ABL == 10 || MC_ABL == 12))
-#ifdef MC_OBS_SLOW
-  if constexpr (false) {
-#else
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&
                 ObsFast<SH::EGO, SH::N, SH::LC>::NB <= CtxT::LPE) {
-#endif
     write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the wave
   } else {
     if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
   }
-#endif
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
     uint8_t* ad = adj_out + (size_t)e * N * N;
@@ -1627,66 +1571,76 @@ static bool getenv_spec() {
   return on;
 }
 
-hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
-                      const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
-                      uint8_t* adj, int nt, int epw, hipStream_t stream) {
+// One env-kernel instantiation: its name (mc_kernel_variant) and launcher.
+struct EnvLaunch {
+  const char* name;
+  void (*launch)(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
+                 const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs, uint8_t* adj,
+                 hipStream_t stream);
+};
+
+template <int T, int P, typename W, class SH>
+static void launch_one(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
+                       const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs, uint8_t* adj,
+                       hipStream_t stream) {
+  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, (int)sizeof(W));
+  hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + P - 1) / P), dim3(T), slot_stride(slot_lds) * P,
+                     stream, s, mode, actions, env_mask, inj_pos, reward, done, obs, adj);
+}
+
+using Dynamic = Shape<0, 0, 0, 0, 0>;
+using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;      // the bench workload
+using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs layers)
+using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;    // 360 beams, R=20
+using ShapeC5 = Shape<16, 10, 21, 0, 10, 8>;     // 16 agents, dist_reward (4 obs layers)
+
+#define MC_EL(T, P, W, SH, NAME) \
+  EnvLaunch { "env_kernel<" #T "," #P "," NAME ">", &launch_one<T, P, W, SH> }
+
+// The instantiation for this state: compiled shapes when the runtime State
+// matches one exactly (and its map offsets fit 32 bits), else the generic
+// kernel for the lane count / envs per workgroup.
+EnvLaunch select_env(const State& s, int nt, int epw) {
   const bool narrow = s.TW <= 4;  // window rows fit a u32
-  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, narrow ? 4 : 8);
-#define MC_LAUNCH_SH(T, P, W, SH)                                                              \
-  hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + (P)-1) / (P)), dim3(T),             \
-                     slot_stride(slot_lds) * (P), stream, s, mode, actions, env_mask, inj_pos,    \
-                     reward, done,                                                               \
-                     obs, adj)
-#define MC_LAUNCH(T, P, W) MC_LAUNCH_SH(T, P, W, Dynamic)
-  using Dynamic = Shape<0, 0, 0, 0, 0>;
   // compiled shapes address the map arrays with 32-bit byte offsets
   const uint64_t mtb = (uint64_t)s.MT * 8;
   const bool fits32 = (uint64_t)s.B * s.N * mtb < (1ull << 32) && (uint64_t)s.G * mtb < (1ull << 32);
-  using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;    // the bench workload
-  using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs layers)
-  using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;  // 360 beams, R=20
-  using ShapeC5 = Shape<16, 10, 21, 0, 10, 8>;   // 16 agents, dist_reward (4 obs layers)
+  const bool spec = getenv_spec();
   if (epw == 2) {
-    if (narrow && fits32 && getenv_spec() && ShapeC2::matches(s)) MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2);
-    else if (narrow && fits32 && getenv_spec() && ShapeC2D::matches(s))
-      MC_LAUNCH_SH(64, 2, uint32_t, ShapeC2D);
-    else if (narrow) MC_LAUNCH(64, 2, uint32_t);
-    else MC_LAUNCH(64, 2, uint64_t);
-  } else if (narrow) {
-    if (nt == 64 && fits32 && getenv_spec() && ShapeC2::matches(s)) {
-      MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2);
-      return hipGetLastError();
-    }
-    if (nt == 64 && fits32 && getenv_spec() && ShapeC2D::matches(s)) {
-      MC_LAUNCH_SH(64, 1, uint32_t, ShapeC2D);
-      return hipGetLastError();
-    }
-    if (nt == 128 && getenv_spec() && ShapeC5::matches(s)) {
-      MC_LAUNCH_SH(128, 1, uint32_t, ShapeC5);
-      return hipGetLastError();
-    }
+    if (narrow && fits32 && spec && ShapeC2::matches(s)) return MC_EL(64, 2, uint32_t, ShapeC2, "u32,C2");
+    if (narrow && fits32 && spec && ShapeC2D::matches(s)) return MC_EL(64, 2, uint32_t, ShapeC2D, "u32,C2D");
+    if (narrow) return MC_EL(64, 2, uint32_t, Dynamic, "u32,generic");
+    return MC_EL(64, 2, uint64_t, Dynamic, "u64,generic");
+  }
+  if (narrow) {
+    if (nt == 64 && fits32 && spec && ShapeC2::matches(s)) return MC_EL(64, 1, uint32_t, ShapeC2, "u32,C2");
+    if (nt == 64 && fits32 && spec && ShapeC2D::matches(s)) return MC_EL(64, 1, uint32_t, ShapeC2D, "u32,C2D");
+    if (nt == 128 && spec && ShapeC5::matches(s)) return MC_EL(128, 1, uint32_t, ShapeC5, "u32,C5");
     switch (nt) {
-      case 64: MC_LAUNCH(64, 1, uint32_t); break;
-      case 128: MC_LAUNCH(128, 1, uint32_t); break;
-      case 256: MC_LAUNCH(256, 1, uint32_t); break;
-      case 512: MC_LAUNCH(512, 1, uint32_t); break;
-      default: MC_LAUNCH(1024, 1, uint32_t); break;
-    }
-  } else {
-    if (nt == 256 && fits32 && getenv_spec() && ShapeC4::matches(s)) {
-      MC_LAUNCH_SH(256, 1, uint64_t, ShapeC4);
-      return hipGetLastError();
-    }
-    switch (nt) {
-      case 64: MC_LAUNCH(64, 1, uint64_t); break;
-      case 128: MC_LAUNCH(128, 1, uint64_t); break;
-      case 256: MC_LAUNCH(256, 1, uint64_t); break;
-      case 512: MC_LAUNCH(512, 1, uint64_t); break;
-      default: MC_LAUNCH(1024, 1, uint64_t); break;
+      case 64: return MC_EL(64, 1, uint32_t, Dynamic, "u32,generic");
+      case 128: return MC_EL(128, 1, uint32_t, Dynamic, "u32,generic");
+      case 256: return MC_EL(256, 1, uint32_t, Dynamic, "u32,generic");
+      case 512: return MC_EL(512, 1, uint32_t, Dynamic, "u32,generic");
+      default: return MC_EL(1024, 1, uint32_t, Dynamic, "u32,generic");
     }
   }
-#undef MC_LAUNCH
-#undef MC_LAUNCH_SH
+  if (nt == 256 && fits32 && spec && ShapeC4::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4, "u64,C4");
+  switch (nt) {
+    case 64: return MC_EL(64, 1, uint64_t, Dynamic, "u64,generic");
+    case 128: return MC_EL(128, 1, uint64_t, Dynamic, "u64,generic");
+    case 256: return MC_EL(256, 1, uint64_t, Dynamic, "u64,generic");
+    case 512: return MC_EL(512, 1, uint64_t, Dynamic, "u64,generic");
+    default: return MC_EL(1024, 1, uint64_t, Dynamic, "u64,generic");
+  }
+}
+#undef MC_EL
+
+const char* env_variant(const State& s, int nt, int epw) { return select_env(s, nt, epw).name; }
+
+hipError_t launch_env(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
+                      const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs,
+                      uint8_t* adj, int nt, int epw, hipStream_t stream) {
+  select_env(s, nt, epw).launch(s, mode, actions, env_mask, inj_pos, reward, done, obs, adj, stream);
   return hipGetLastError();
 }
 

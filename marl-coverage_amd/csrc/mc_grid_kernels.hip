@@ -110,7 +110,7 @@ __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int al
     for (int r = 0; r < 8; ++r) {
       const int x = 8 * ti + r;
       for (int h = 0; h < 2; ++h) {
-        const uint4 q = philox(seed, make_uint4((uint32_t)g, (uint32_t)x, (uint32_t)(tj * 2 + h), 0x67656e21u));
+        const uint4 q = philox(seed, make_uint4(s.grid0 + (uint32_t)g, (uint32_t)x, (uint32_t)(tj * 2 + h), 0x67656e21u));
         const uint32_t rv[4] = {q.x, q.y, q.z, q.w};
         for (int t = 0; t < 4; ++t) {
           const int c = h * 4 + t;
@@ -126,6 +126,24 @@ __global__ void gen_grids_kernel(State s, uint64_t seed, uint32_t thresh, int al
     const_cast<uint64_t*>(s.grid_pos)[i] = pos;
     if (pos) atomicAdd(const_cast<int32_t*>(&s.numfree[g]), (int32_t)__popcll(pos));
   }
+}
+
+// Synthetic actions (SURVEY 8(d) "Actions (GPU)"): agent i of env e at step
+// t is bits 2i, 2i+1 of Philox(seed, (global env id, t)) -- one 128-bit draw
+// per env covers N <= 64 agents.
+__global__ void random_actions_kernel(State s, uint64_t seed, uint32_t step, uint8_t* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.B) return;
+  const uint4 r = philox(seed, make_uint4(s.env0 + (uint32_t)e, step, 0u, 0x61637473u));
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint8_t* o = out + (size_t)e * s.N;
+  for (int i = 0; i < s.N; ++i) o[i] = (uint8_t)((w[i >> 4] >> (2 * (i & 15))) & 3u);
+}
+
+hipError_t launch_random_actions(const State& s, uint64_t seed, int step, uint8_t* out, hipStream_t stream) {
+  hipLaunchKernelGGL(random_actions_kernel, dim3((s.B + 255) / 256), dim3(256), 0, stream, s, seed,
+                     (uint32_t)step, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_share(const State& s, const uint8_t* actions, hipStream_t stream) {

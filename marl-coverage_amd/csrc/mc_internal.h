@@ -65,6 +65,7 @@ struct State {
   int maxsteps, comm_r, sst, auto_reset, grid_mode;
   int dist;                // dist_reward: add the pre-sense distance terms
   uint64_t seed;
+  uint32_t env0, grid0;     // global ids of env 0 / pool grid 0 (mc_config env_offset / grid_offset)
 
   const uint64_t* grid_neg;
   const uint64_t* grid_pos;

@@ -67,9 +67,9 @@ struct SState {
   int32_t* dist_M; // [B] max(d) of the layer as last written (-1 unknown, -2 no source)
   double* ep_pc;   // [B] episode record at done (before an auto-reset): percent_covered()
   int32_t* ep_len; // [B] ... and _currstep
-  int abl;  // timing ablations (MARLCOV_SG_ABL, results invalid): 1 no sense, 2 no phase B, 4 no moves
   uint32_t mg_L;  // floor(i / L) == umulhi(i, mg_L) (L >= 2)
   uint64_t seed;
+  uint32_t env0, grid0;   // global ids of env 0 / pool grid 0 (mc_sg_config)
   const uint64_t* gneg;   // [G][W][RW] grid < 0
   const uint64_t* gpos;   // [G][W][RW] grid > 0
   const int32_t* numpos;  // [G] count_nonzero(grid > 0)
@@ -161,7 +161,7 @@ __device__ void sg_reset_env(const SState& s, int e, int lane, const int32_t* in
   const uint32_t ep = s.episode[e] + 1u;
   int g = s.env_grid[e];
   if (s.grid_mode == 1) {
-    const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, (uint32_t)e, ep, 0x53677264u));
+    const uint4 r = philox(s.seed, make_uint4(0xFFFFFFFFu, s.env0 + (uint32_t)e, ep, 0x53677264u));
     g = (int)bounded(r.x, (uint32_t)s.G);
   }
   const size_t mw = (size_t)s.W * s.RW;
@@ -186,7 +186,7 @@ __device__ void sg_reset_env(const SState& s, int e, int lane, const int32_t* in
     int placed = 0;
     for (int round = 0; round < 4096 && placed < N; ++round) {
       const uint32_t k = (uint32_t)(round * 64 + lane);
-      const uint4 r = philox(s.seed, make_uint4(k, (uint32_t)e, ep, 0x53706c63u));
+      const uint4 r = philox(s.seed, make_uint4(k, s.env0 + (uint32_t)e, ep, 0x53706c63u));
       const int cx = (int)bounded(r.x, (uint32_t)s.W);
       const int cy = (int)bounded(r.y, (uint32_t)s.L);
       uint64_t okm = __ballot(!bit_at(gneg, s.RW, cx, cy));
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
       gfree = inb && !bit_at(gneg, RW, tx, ty);
     }
     double v = 0.0;
-    for (int k = 0; k < ((s.abl & 4) ? 0 : N); ++k) {  // slot order; robot z = the one with slot k
+    for (int k = 0; k < N; ++k) {  // slot order; robot z = the one with slot k
       const int z = s.scan ? (__ffsll((unsigned long long)__ballot(me && slot == k)) - 1) : k;
       const int zu = __shfl(u, z);
       if (zu >= 4) continue;  // not a move: nothing happens (no penalty)
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
       }
     };
     int cnt = 0;
-    if (me && !(s.abl & 1)) {
+    if (me) {
 #pragma unroll kRowUnroll
       for (int jj = 0; jj < (R >= 0 ? 2 * R + 1 : n); ++jj) {
         const int j = x - r + jj;
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     // phase B: maps (idempotent ORs of the whole window) and state planes
     const size_t WL = (size_t)W * L;
     uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
-    if (me && !(s.abl & 2)) {
+    if (me) {
       uint8_t* pl_obst = pl + (size_t)s.P * WL;
       uint8_t* pl_free = pl + (size_t)(s.P + 1) * WL;
 #pragma unroll kRowUnroll
@@ -762,7 +762,7 @@ __global__ void sg_gen_kernel(SState s, uint64_t seed, uint32_t thresh, uint64_t
     const int nb = min(64, s.L - wv * 64);
     uint64_t neg = 0;
     for (int q = 0; q < 16; ++q) {
-      const uint4 r = philox(seed, make_uint4((uint32_t)x, (uint32_t)wv, (uint32_t)g, 0x5367656eu + ((uint32_t)q << 28)));
+      const uint4 r = philox(seed, make_uint4((uint32_t)x, (uint32_t)wv, s.grid0 + (uint32_t)g, 0x5367656eu + ((uint32_t)q << 28)));
       neg |= (uint64_t)(r.x < thresh) << (4 * q);
       neg |= (uint64_t)(r.y < thresh) << (4 * q + 1);
       neg |= (uint64_t)(r.z < thresh) << (4 * q + 2);
@@ -927,12 +927,12 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   s.grid_mode = c.reset_grid_mode;
   s.mg_L = mc::magic_div((uint32_t)c.length);
   {
-    const char* ab = getenv("MARLCOV_SG_ABL");
-    s.abl = ab ? atoi(ab) : 0;
     const char* fd = getenv("MARLCOV_SG_FULL_DIST");
     s.dist_full = fd && atoi(fd) == 1;
   }
   s.seed = c.seed;
+  s.env0 = c.env_offset;
+  s.grid0 = c.grid_offset;
   // distance planes: u16 rows with an odd dword pitch (the row pass writes
   // column v of W rows at once: distinct banks)
   E->pitch = ((c.length + 1) / 2) * 2;

@@ -107,31 +107,32 @@ class DecGridRL:
         new object every time."""
         shape = np.asarray(raw).shape
         padded_shape = (shape[0] + 2, shape[1] + 2)
-        uniq = self._envs[padded_shape][1] if padded_shape in self._envs else None
-        if uniq is None:
-            uniq, seen = [], set()
-            for g in list(self._train_gridlis or []) + list(self._test_gridlis or []):
-                if id(g) not in seen and np.asarray(g).shape == shape:
-                    seen.add(id(g))
-                    uniq.append(g)
         hit = self._pool_index.get(id(raw))
-        if (padded_shape not in self._envs or hit is None or hit[0] != padded_shape
-                or uniq[hit[1]] is not raw):
-            if not any(g is raw for g in uniq):
-                # a grid outside the train/test lists (e.g. a list entry the
-                # caller replaced): the pool of its shape grows by one
-                uniq = uniq + [raw]
-            if padded_shape in self._envs:
-                self._envs.pop(padded_shape)[0].close()
-                if self._env is not None and self._env._h is None:
-                    self._env = None
-            env = BatchCoverageEnv(self._env_config, 1, grids=[np.asarray(g) for g in uniq],
-                                   device=self._device, auto_reset=False, sensor=self._sensor,
-                                   want_adjacency=True)
-            self._envs[padded_shape] = (env, uniq)
-            self._pool_index.update({id(g): (padded_shape, i) for i, g in enumerate(uniq)})
-            hit = self._pool_index[id(raw)]
-        return self._envs[padded_shape][0], hit[1]
+        if (padded_shape in self._envs and hit is not None and hit[0] == padded_shape
+                and self._envs[padded_shape][1][hit[1]] is raw):
+            return self._envs[padded_shape][0], hit[1]
+        # a miss: the pool of this shape is rebuilt from the CURRENT train /
+        # test lists (entries the caller replaced drop out, so the pool does
+        # not grow with every replacement), plus ``raw`` if it is in neither
+        uniq, seen = [], set()
+        for g in list(self._train_gridlis or []) + list(self._test_gridlis or []):
+            if id(g) not in seen and np.asarray(g).shape == shape:
+                seen.add(id(g))
+                uniq.append(g)
+        if id(raw) not in seen:
+            uniq.append(raw)
+        if padded_shape in self._envs:
+            self._envs.pop(padded_shape)[0].close()
+            if self._env is not None and self._env._h is None:
+                self._env = None
+        env = BatchCoverageEnv(self._env_config, 1, grids=[np.asarray(g) for g in uniq],
+                               device=self._device, auto_reset=False, sensor=self._sensor,
+                               want_adjacency=True)
+        self._envs[padded_shape] = (env, uniq)
+        # forget the evicted grids of this shape (ids of dead objects get reused)
+        self._pool_index = {k: v for k, v in self._pool_index.items() if v[0] != padded_shape}
+        self._pool_index.update({id(g): (padded_shape, i) for i, g in enumerate(uniq)})
+        return env, self._pool_index[id(raw)][1]
 
     def _push_done_thresh(self, env):
         t = self._torch.tensor([float(self._dt)], dtype=self._torch.float64)

@@ -48,13 +48,22 @@ class Sensor:
         self._listeners = [w for w in self._listeners if w() is not None and w() != bound_method]
 
     def _changed(self):
-        live = []
+        """Call every live listener (all of them, even after one fails: a
+        shared sensor must not leave its envs on different tables), prune the
+        dead ones, then re-raise the first failure."""
+        live, err = [], None
         for w in self._listeners:
             fn = w()
-            if fn is not None:
-                live.append(w)
+            if fn is None:
+                continue
+            live.append(w)
+            try:
                 fn(self)
+            except Exception as e:  # noqa: BLE001 -- re-raised below
+                err = err or e
         self._listeners = live
+        if err is not None:
+            raise err
 
 
 class LidarSensor(Sensor):
@@ -73,10 +82,19 @@ class LidarSensor(Sensor):
 
     def set_thetalist(self, thetalist):
         """Replace the beam angles (any count); pushes the new table to every
-        device env built on this sensor."""
+        device env built on this sensor.  If a device env rejects the table
+        (mc_set_beam_table validates before it changes anything), the old
+        angles are restored and pushed to every env again, then the error is
+        raised: sensor, configs and devices never disagree."""
+        old = (self._thetalist, self._num_lasers)
         self._thetalist = np.asarray(thetalist, dtype=np.float64)
         self._num_lasers = len(self._thetalist)
-        self._changed()
+        try:
+            self._changed()
+        except Exception:
+            self._thetalist, self._num_lasers = old
+            self._changed()
+            raise
 
     def table(self) -> np.ndarray:
         return beam_increments(self._thetalist)

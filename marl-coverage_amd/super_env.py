@@ -61,7 +61,8 @@ class BatchSuperGridEnv:
     """
 
     def __init__(self, env_config, num_envs, grids=None, *, gen=None, device="cuda", seed=0,
-                 auto_reset=True, maxsteps=0, reset_grid_mode="keep", env_grid=None):
+                 auto_reset=True, maxsteps=0, reset_grid_mode="keep", env_grid=None, env_offset=0,
+                 grid_offset=None):
         import torch
 
         self._torch = torch
@@ -103,6 +104,8 @@ class BatchSuperGridEnv:
         c.auto_reset = int(bool(auto_reset))
         c.reset_grid_mode = {"keep": 0, "random": 1}[reset_grid_mode]
         c.seed = int(seed) & (2 ** 64 - 1)
+        c.env_offset = int(env_offset)  # global ids (BatchCoverageEnv)
+        c.grid_offset = int(env_offset if grid_offset is None else grid_offset)
         self._cfg = c
         h = ctypes.c_void_p()
         _lib.check(self.lib.mc_sg_create(ctypes.byref(c), dev.index, ctypes.byref(h)), "mc_sg_create")

@@ -13,25 +13,44 @@ def unpack_tiles(tiles, rows, cols):
     return tiles_to_cells(tiles, rows, cols)
 
 
-def device_state(env):
-    """Host copies of every per-env state field of a BatchCoverageEnv."""
+def device_state(env, envs=None):
+    """Host copies of every per-env state field of a BatchCoverageEnv.  With
+    ``envs`` (a list of env indices) the bit maps are unpacked only for those
+    envs (and their grids) and come back as dicts keyed by env / grid index:
+    C5-sized batches would otherwise unpack gigabytes per step."""
     from marlcov import _lib
     W, L = env.width, env.length
+
+    def get(f):
+        return env.get_state(f).cpu().numpy()
+
     st = {
-        "pos": env.get_state(_lib.FIELD_POS).cpu().numpy(),
-        "moved": env.get_state(_lib.FIELD_MOVED).cpu().numpy().astype(np.uint64),
-        "free": unpack_tiles(env.get_state(_lib.FIELD_FREE).cpu().numpy(), W, L),
-        "obst": unpack_tiles(env.get_state(_lib.FIELD_OBST).cpu().numpy(), W, L),
-        "vis": unpack_tiles(env.get_state(_lib.FIELD_VISITED).cpu().numpy(), W, L),
-        "free_cnt": env.get_state(_lib.FIELD_FREE_COUNT).cpu().numpy(),
-        "vis_cnt": env.get_state(_lib.FIELD_VISITED_COUNT).cpu().numpy(),
-        "currstep": env.get_state(_lib.FIELD_CURRSTEP).cpu().numpy(),
-        "done_thresh": env.get_state(_lib.FIELD_DONE_THRESH).cpu().numpy(),
-        "env_grid": env.get_state(_lib.FIELD_ENV_GRID).cpu().numpy(),
-        "neg": unpack_tiles(env.get_state(_lib.FIELD_GRID_NEG).cpu().numpy(), W, L),
-        "pos_plane": unpack_tiles(env.get_state(_lib.FIELD_GRID_POS).cpu().numpy(), W, L),
-        "numfree": env.get_state(_lib.FIELD_NUMFREE).cpu().numpy(),
+        "pos": get(_lib.FIELD_POS),
+        "moved": get(_lib.FIELD_MOVED).astype(np.uint64),
+        "free_cnt": get(_lib.FIELD_FREE_COUNT),
+        "vis_cnt": get(_lib.FIELD_VISITED_COUNT),
+        "currstep": get(_lib.FIELD_CURRSTEP),
+        "done_thresh": get(_lib.FIELD_DONE_THRESH),
+        "env_grid": get(_lib.FIELD_ENV_GRID),
+        "episode": get(_lib.FIELD_EPISODE),
+        "numfree": get(_lib.FIELD_NUMFREE),
     }
+    maps = {"free": _lib.FIELD_FREE, "obst": _lib.FIELD_OBST, "vis": _lib.FIELD_VISITED}
+    grids = {"neg": _lib.FIELD_GRID_NEG, "pos_plane": _lib.FIELD_GRID_POS}
+    if envs is None:
+        for k, f in {**maps, **grids}.items():
+            st[k] = unpack_tiles(get(f), W, L)
+        return st
+    envs = [int(b) for b in envs]
+    gids = sorted({int(st["env_grid"][b]) for b in envs})
+    for k, f in maps.items():
+        t = env.get_state(f)
+        sel = unpack_tiles(t[envs].cpu().numpy(), W, L)
+        st[k] = {b: sel[i] for i, b in enumerate(envs)}
+    for k, f in grids.items():
+        t = env.get_state(f)
+        sel = unpack_tiles(t[gids].cpu().numpy(), W, L)
+        st[k] = {g: sel[i] for i, g in enumerate(gids)}
     return st
 
 

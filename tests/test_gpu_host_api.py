@@ -43,7 +43,7 @@ def test_list_grids_many_resets_match_oracle(torch_cuda):
     np.random.seed(3)
     ref = DecGridRLRef(train, c)
     for ep in range(8):
-        if ep == 5:
+        if ep in (3, 5, 6):
             train[1] = mk(12, 12)  # a new object of an existing shape
         seed = 100 + ep
         np.random.seed(seed)
@@ -60,6 +60,11 @@ def test_list_grids_many_resets_match_oracle(torch_cuda):
             assert float(r) == float(rr), tag
             assert bool(d) == bool(rd), tag
             np.testing.assert_array_equal(o, ro, err_msg=tag)
+    # replaced entries leave the pool at the next rebuild: it never grows past
+    # the lists' two 12x12 grids
+    pool = env._envs[(14, 14)][1]
+    assert len(pool) == 2 and pool[0] is train[0]
+    assert sum(v[0] == (14, 14) for v in env._pool_index.values()) == 2
 
 
 def test_shared_sensor_does_not_keep_envs_alive(torch_cuda):
@@ -84,7 +89,16 @@ def test_beam_table_over_lds_budget_is_rejected(torch_cuda):
     checked is refused when the table is set, with a clear error."""
     import marlcov
     env = marlcov.BatchCoverageEnv(cfg(), 1, grids=[np.ones((20, 20))])
+    other = marlcov.BatchCoverageEnv(cfg(), 1, grids=[np.ones((20, 20))], sensor=env.sensor)
+    n0 = env.sensor._num_lasers
     with pytest.raises(Exception, match="LDS"):  # 16 B per beam: 4500 beams > 64 KiB
         env.sensor.set_thetalist(np.linspace(0, 2 * np.pi, 4500, endpoint=False))
-    env.reset()
-    env.check()
+    # the old table is still the one in effect everywhere
+    assert env.sensor._num_lasers == n0 and len(env.sensor._thetalist) == n0
+    assert env._cfg.num_beams == n0 and other._cfg.num_beams == n0
+    for e in (env, other):
+        e.reset(positions=np.array([[[5, 5], [7, 9]]], dtype=np.int32))
+        e.check()
+    # the shared sensor's two envs see the same cells after the rejection
+    assert env.obs.cpu().numpy().tobytes() == other.obs.cpu().numpy().tobytes()
+    assert len(env.sensor._listeners) == 2

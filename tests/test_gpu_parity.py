@@ -206,14 +206,16 @@ def test_batch_matches_oracle(torch_cuda, name):
     env.check()
 
 
-def check_dist_mw(env, refs, tag):
+def check_dist_mw(env, refs, tag, envs=None):
     """Every known (M, witness) of the device equals the oracle's fresh
-    distance transform: M = its max, d(witness) = M."""
+    distance transform: M = its max, d(witness) = M.  ``refs``: a list (env
+    b = refs[b]) or a dict {b: oracle env}."""
     from marlcov import _lib
     from oracle.cpu_ref import l1_distance_to_covered
     mw = env.get_state(_lib.FIELD_DIST_MW).cpu().numpy()
     known = 0
-    for b, ref in enumerate(refs):
+    items = refs.items() if isinstance(refs, dict) else enumerate(refs)
+    for b, ref in items:
         p = ref._pad
         for i in range(ref._numrobot):
             M, w = int(mw[b, i, 0]), int(mw[b, i, 1])
@@ -317,7 +319,7 @@ def test_c2_full_size_invariants_and_sampled_parity(torch_cuda):
         acts = rs.randint(0, 4, size=(B, 4)).astype(np.uint8)
         obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
         obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
-        st = device_state(env)
+        st = device_state(env, sample)
         for b in sample:
             o, r, d = refs[b].step(acts[b].astype(np.int64))
             assert float(r) == rew_h[b] and bool(d) == bool(done_h[b]), (t, b)
@@ -326,40 +328,6 @@ def test_c2_full_size_invariants_and_sampled_parity(torch_cuda):
                 o, _ = refs[b].reset(False, None, positions=[tuple(x) for x in q])
             np.testing.assert_array_equal(obs_h[b], o)
             compare_env(st, b, refs[b], f"c2 t={t} env {b}")
-
-
-def test_c5_dist_sampled_parity(torch_cuda):
-    """BASELINE configs[4] shape (16 agents, 512x512, dist_reward) on 256 envs:
-    after 40 steps of incremental max(d) tracking, envs re-built in the oracle
-    from the device maps (fresh distance transforms) step on bit-exactly."""
-    import marlcov
-    torch = torch_cuda
-    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=2000)
-    B = 256
-    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
-                                   seed=5, auto_reset=True)
-    env.reset()
-    g = torch.Generator(device=env.device)
-    g.manual_seed(0)
-    for t in range(40):
-        acts = torch.randint(0, 4, (B, 16), dtype=torch.uint8, device=env.device, generator=g)
-        env.step(acts)
-    torch.cuda.synchronize()
-    env.check()
-    st = device_state(env)
-    sample = [3, 101, 200]
-    refs = {b: oracle_from_device(st, b, cfg) for b in sample}
-    rs = np.random.RandomState(12)
-    for t in range(4):
-        acts = rs.randint(0, 4, size=(B, 16)).astype(np.uint8)
-        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
-        obs_h, rew_h = full_obs(env, obs, cfg), rew.cpu().numpy()
-        st = device_state(env)
-        for b in sample:
-            o, r, d = refs[b].step(acts[b].astype(np.int64))
-            assert float(r) == rew_h[b], (t, b, float(r), rew_h[b])
-            np.testing.assert_array_equal(obs_h[b], o, err_msg=f"c5 t={t} env {b}")
-            compare_env(st, b, refs[b], f"c5 t={t} env {b}")
 
 
 def test_determinism_same_seed(torch_cuda):

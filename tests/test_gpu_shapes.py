@@ -1,0 +1,213 @@
+"""GPU parity of the compiled-shape kernels the benchmark times.
+
+The env kernel is instantiated per BASELINE workload shape (csrc/
+mc_env_kernel.hip select_env: C2, C2D = C2 + dijkstra_input, C4, C5); every
+other config runs the generic instantiation.  These tests run each compiled
+shape — asserted through mc_kernel_variant — against the oracle
+(oracle/cpu_ref.py) every step, including the auto-reset branch inside the
+kernel (dec_grid_rl.py:449-531 reached from done() :533-546) and the distance
+transform instantiations (csrc/mc_dist.hip dist_kernel_t<16/33/52>).  Device
+start cells of every reset are also checked against the host restatement of
+the device Philox stream (marlcov.streams.start_cells), and the sharded-batch
+property of SURVEY 8(e) (env e's trajectory does not depend on the shard it
+runs in) is checked on one GPU with two handles.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from gpu_util import compare_env, device_state, oracle_from_device, ref_action
+from test_gpu_parity import base_cfg, bern, check_dist_mw, full_obs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+def _actions(rs, B, N, sentinel_p=0.05, noop_p=0.06):
+    acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+    acts[rs.rand(B, N) < noop_p] = rs.choice([4, 9, 254])
+    acts[rs.rand(B) < sentinel_p, 0] = 255
+    return acts
+
+
+def run_against_oracle(torch, env, cfg, rs, T, envs, seed, label, dist_check=False, sentinel_p=0.05):
+    """Step ``env`` T times with random actions (no-op codes and sentinel rows
+    included) and compare the envs in ``envs`` with oracle envs rebuilt from
+    the device state after the reset: reward, done, obs (with the float dist
+    layer), positions, maps, counters every step; on every done the oracle
+    resets at the device-drawn cells, which must equal the host Philox draw.
+    Returns the number of auto-resets seen."""
+    from marlcov import streams
+    B, N = env.num_envs, env.num_agents
+    st = device_state(env, envs)
+    refs = {b: oracle_from_device(st, b, cfg) for b in envs}
+    resets = 0
+    for t in range(T):
+        acts = _actions(rs, B, N, sentinel_p=sentinel_p)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env, envs)
+        for b in envs:
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"{label} t={t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            assert bool(d) == bool(done_h[b]), tag
+            if d:
+                resets += 1
+                p = st["pos"][b]
+                g = int(st["env_grid"][b])
+                grid = np.where(st["neg"][g] == 1, -1.0, np.where(st["pos_plane"][g] == 1, 1.0, 0.0))
+                want = streams.start_cells(seed, env.env_offset + b, int(st["episode"][b]), grid, N)
+                np.testing.assert_array_equal(p, want, err_msg=tag + " start cells vs host Philox")
+                o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in p])
+                assert int(st["currstep"][b]) == 0, tag
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+        if dist_check:
+            check_dist_mw(env, refs, f"{label} t={t}", envs=envs)
+    env.check()
+    return resets
+
+
+# (config, unpadded grid side, envs, steps, expected variant tag)
+SHAPES = {
+    "C2": (base_cfg(numrobot=4, maxsteps=7), 40, 16, 30, "C2"),
+    "C2D": (base_cfg(numrobot=4, maxsteps=7, dijkstra_input=1), 40, 16, 30, "C2D"),
+    "C4": (base_cfg(numrobot=8, maxsteps=7, allow_even_beams=True, sensor_config={"num_lasers": 360, "range": 20}),
+           60, 6, 20, "C4"),
+    "C5": (base_cfg(numrobot=16, maxsteps=7, dist_reward=1), 40, 6, 20, "C5"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_compiled_shape_auto_reset(torch_cuda, name):
+    """Every compiled shape with auto_reset and a short episode (maxsteps 7):
+    done envs reset inside the step kernel (its reset_env instantiation) and
+    the new episode equals the oracle's reset at the device-drawn cells."""
+    import marlcov
+    torch = torch_cuda
+    cfg, side, B, T, tag = SHAPES[name]
+    rs = np.random.RandomState(zlib.crc32(name.encode()))
+    grids = [bern(rs, side, side, 0.1) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=True, seed=77, env_offset=1000)
+    assert f",{tag}>" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    resets = run_against_oracle(torch, env, cfg, rs, T, list(range(B)), 77, name,
+                                dist_check=bool(cfg.get("dist_reward")))
+    assert resets >= B  # maxsteps=7 over >= 20 steps: every env reset at least twice, less sentinels
+
+
+def test_c4_shape_256_many_envs(torch_cuda):
+    """BASELINE configs[3] geometry (8 agents, 256x256, 360 beams, R=20) on
+    16 envs x 40 steps through the C4 instantiation, with auto-resets (maxsteps
+    13).  360 beams never share one step pattern over every start (mc_set_beam_table:
+    beam_common is off), so the march reads the per-start beam table."""
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=8, maxsteps=13, allow_even_beams=True, sensor_config={"num_lasers": 360, "range": 20})
+    rs = np.random.RandomState(404)
+    B = 16
+    grids = [bern(rs, 256, 256, 0.1) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=True, seed=5)
+    assert ",C4>" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    resets = run_against_oracle(torch, env, cfg, rs, 40, list(range(B)), 5, "c4_256", sentinel_p=0.02)
+    assert resets >= B
+
+
+def test_c5_shape_512_per_step(torch_cuda):
+    """BASELINE configs[4] geometry (16 agents, 512x512, dist_reward) on 256
+    envs through the C5 instantiation: 8 envs compared with the oracle every
+    step from the reset for 30 steps, and every known (max d, witness) of those
+    envs checked against a fresh transform every step.  RX = 518 extended rows
+    runs the full transform as dist_kernel_t<33> (mc_dist.hip chunk_rows)."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=2000)
+    B = 256
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
+                                   seed=5, auto_reset=True)
+    assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+    assert env.width + 2 * env.pad == 518
+    env.reset()
+    assert int(env.get_state(_lib.FIELD_DIST_LISTED).item()) > 0  # reset: M unknown, full transforms
+    sample = [0, 17, 64, 101, 150, 200, 233, 255]
+    rs = np.random.RandomState(12)
+    run_against_oracle(torch, env, cfg, rs, 30, sample, 5, "c5_512", dist_check=True, sentinel_p=0.0)
+
+
+def test_dist_kernel_52_rows(torch_cuda):
+    """Extended maps of 529..832 rows run the transform as dist_kernel_t<52>:
+    a 600 x 40 grid (RX = 606) with dist_reward, per step against the oracle."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=2, dist_reward=1, sensor_config={"num_lasers": 9, "range": 4})
+    rs = np.random.RandomState(52)
+    B = 4
+    grids = [bern(rs, 600, 40, 0.1) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False)
+    assert 529 <= env.width + 2 * env.pad <= 832
+    env.reset()
+    assert int(env.get_state(_lib.FIELD_DIST_LISTED).item()) > 0
+    run_against_oracle(torch, env, cfg, rs, 20, list(range(B)), 0, "dist52", dist_check=True, sentinel_p=0.0)
+
+
+# ---------------------------------------------------------------------------
+# every device stream keyed by the global env id
+# ---------------------------------------------------------------------------
+def test_shards_reproduce_one_batch(torch_cuda):
+    """Two handles holding envs [0, B) and [B, 2B) of a global batch (env
+    offsets 0 and B) reproduce one 2B handle bit for bit over 50 auto-reset
+    steps at the C2 shape: grids (mc_generate_grids), start cells, actions
+    (mc_random_actions), obs, rewards, dones and maps.  The grids, the first
+    start cells and the actions also equal the host restatement of the
+    streams (marlcov.streams)."""
+    import marlcov
+    from marlcov import _lib, streams
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=4, maxsteps=9)
+    B, S = 64, 50
+    gen = dict(width=64, length=64, prob_obst=0.1, seed=1000)
+
+    def make(n, off):
+        e = marlcov.BatchCoverageEnv(cfg, n, gen=dict(gen, num_grids=n), seed=1, auto_reset=True,
+                                     env_offset=off)
+        e.reset()
+        return e
+
+    whole, lo, hi = make(2 * B, 0), make(B, 0), make(B, B)
+    assert ",C2>" in whole.kernel_variant()
+    # host restatement of the grid pool and the first start cells
+    st = device_state(whole, [0, 5, B + 3])
+    for b in (0, 5, B + 3):
+        want = streams.generated_grid(1000, 0.1, 66, 66, b)
+        got = np.where(st["neg"][b] == 1, -1.0, 1.0)
+        np.testing.assert_array_equal(got, want, err_msg=f"grid {b}")
+        np.testing.assert_array_equal(st["pos"][b], streams.start_cells(1, b, 1, want, 4), err_msg=f"cells {b}")
+    for t in range(S):
+        a_w = whole.random_actions(12345, t)
+        a_l, a_h = lo.random_actions(12345, t), hi.random_actions(12345, t)
+        assert torch.equal(a_w, torch.cat([a_l, a_h]))
+        if t in (0, 17):
+            np.testing.assert_array_equal(a_w.cpu().numpy(), streams.random_actions(12345, range(2 * B), t, 4))
+        ow, rw, dw = whole.step(a_w)
+        ol, rl, dl = lo.step(a_l)
+        oh, rh, dh = hi.step(a_h)
+        assert torch.equal(ow, torch.cat([ol, oh])), t
+        assert torch.equal(rw, torch.cat([rl, rh])) and torch.equal(dw, torch.cat([dl, dh])), t
+    for f in (_lib.FIELD_POS, _lib.FIELD_FREE, _lib.FIELD_OBST, _lib.FIELD_VISITED, _lib.FIELD_EPISODE,
+              _lib.FIELD_FREE_COUNT, _lib.FIELD_CURRSTEP):
+        assert torch.equal(whole.get_state(f), torch.cat([lo.get_state(f), hi.get_state(f)])), f
+    assert int(whole.get_state(_lib.FIELD_EPISODE).min()) >= 5  # maxsteps 9 over 50 steps
+    for e in (whole, lo, hi):
+        e.check()

@@ -278,3 +278,43 @@ def test_sensor_listeners_are_weak():
     s.remove_listener(b.upload)
     s.set_thetalist(np.linspace(0, 2 * np.pi, 3, endpoint=False))
     assert calls == [7, 7, 9] and s._listeners == []
+
+
+def test_philox_known_answers():
+    """marlcov.streams restates the device's Philox4x32-10 (csrc/mc_device.h):
+    pinned to the Random123 known-answer vectors (kat_vectors, philox4x32_10)."""
+    from marlcov.streams import philox4x32_10
+    kat = [
+        ((0, 0, 0, 0), 0, (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+        ((0xFFFFFFFF,) * 4, 0xFFFFFFFFFFFFFFFF, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+        ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), 0x299F31D0A4093822,
+         (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+    ]
+    for ctr, key, want in kat:
+        got = tuple(int(x) for x in philox4x32_10(key, *ctr))
+        assert got == want, (ctr, [hex(x) for x in got])
+
+
+def test_host_streams_shapes_and_rules():
+    """Host mirrors of the device streams: the gen grid has the -1 border and
+    about p_obst obstacles; start cells are distinct free cells; actions are
+    0..3 and depend only on (global env id, step)."""
+    from marlcov.streams import generated_grid, random_actions, start_cells
+    g = generated_grid(1000, 0.1, 130, 130, 7)
+    assert g.shape == (130, 130) and set(np.unique(g)) <= {-1.0, 1.0}
+    assert np.all(g[0] == -1) and np.all(g[-1] == -1) and np.all(g[:, 0] == -1) and np.all(g[:, -1] == -1)
+    frac = np.mean(g[1:-1, 1:-1] < 0)
+    assert 0.08 < frac < 0.12
+    assert not np.array_equal(g, generated_grid(1000, 0.1, 130, 130, 8))
+    cells = start_cells(1, 7, 1, g, 4)
+    assert len({tuple(c) for c in cells}) == 4 and all(g[x, y] >= 0 for x, y in cells)
+    a = random_actions(12345, [3, 4, 5], 9, 16)
+    assert a.shape == (3, 16) and a.max() <= 3
+    np.testing.assert_array_equal(a[1:], random_actions(12345, [4, 5], 9, 16))
+    assert not np.array_equal(a, random_actions(12345, [3, 4, 5], 10, 16))
+
+
+def test_kernel_variant_null_env(lib):
+    assert lib.mc_kernel_variant(None) == b""
+    assert "null" in lib.mc_last_error().decode()
+    assert lib.mc_random_actions(None, 0, 0, None, None) == -1

@@ -1,9 +1,8 @@
 """Build diagnostic variants of libmarlcov.so for A/B runs on the GPU box.
 
     python tools/build_variants.py NAME:FLAGS [NAME:FLAGS ...]
-e.g.  abl1:-DMC_ABL=1  base:   -> marl-coverage_amd/libmarlcov_v_<NAME>.so
-Select one with MARLCOV_LIB=<path> (marlcov/_lib.py).  MC_ABL builds give
-wrong results by design (timing ablations).
+e.g.  stamps:-DMC_STAMPS  base:   -> marl-coverage_amd/libmarlcov_v_<NAME>.so
+Select one with MARLCOV_LIB=<path> (marlcov/_lib.py).
 """
 import glob
 import os

@@ -8,28 +8,20 @@ absolute kernel time.
 """
 import argparse
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "marl-coverage_amd")
 LIB = os.path.join(PKG, "libmarlcov_stamps.so")
-# MC_ABL timing ablations (wrong results): 1 lidar marks to the sink only,
-# 3 no sense, 4 merge without dedup, 5 no obs, 6 stage without the mask loads
-ABLATIONS = (1, 3, 4, 5, 6)
 PHASES = ["rt1 pos/act/scalars", "rt2 stage", "moves", "sense", "merge", "reward",
           "store", "(reset)", "obs", "adj+drain"]
 
 
-def build(abl=None):
-    import glob
-    srcs = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")))
-    out = LIB if abl is None else LIB.replace(".so", f"_abl{abl}.so")
-    extra = [] if abl is None else [f"-DMC_ABL={abl}"]
-    cmd = ["hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared", "-DMC_STAMPS",
-           *extra, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc"), "-o", out, *srcs]
-    subprocess.run(cmd, check=True)
+def build():
+    sys.path.insert(0, PKG)
+    import build as mcbuild  # marl-coverage_amd/build.py
+    mcbuild.build(extra_flags=["-DMC_STAMPS"], out=LIB)
 
 
 def main():
@@ -37,17 +29,12 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--build-only", action="store_true")
-    ap.add_argument("--abl", type=int, default=None, help="timing ablation build (wrong results)")
-    ap.add_argument("--all-abl", action="store_true", help="also build ablations 1..5")
     args = ap.parse_args()
     if args.build_only or not os.path.exists(LIB):
         build()
-        if args.all_abl:
-            for a in ABLATIONS:
-                build(a)
         if args.build_only:
             return
-    os.environ["MARLCOV_LIB"] = LIB if args.abl is None else LIB.replace(".so", f"_abl{args.abl}.so")
+    os.environ["MARLCOV_LIB"] = LIB
     print("library:", os.environ["MARLCOV_LIB"])
     import numpy as np
     import torch
