@@ -107,13 +107,15 @@ class BatchCoverageEnv:
         c.num_agents = self.num_agents
         c.width, c.length = self.width, self.length
         c.num_grids = self.num_grids
-        if isinstance(self.sensor, LidarSensor):
+        if self.sensor.sensor_type == LidarSensor.sensor_type:
             c.sensor_type = _lib.SENSOR_LIDAR
             c.num_beams = self.sensor._num_lasers
             c.lidar_range = float(self.sensor._max_range)
-        elif isinstance(self.sensor, SquareSensor):
+        elif self.sensor.sensor_type == SquareSensor.sensor_type:
             c.sensor_type = _lib.SENSOR_SQUARE
             c.square_radius = self.sensor._radius
+        else:
+            raise ValueError(f"unsupported sensor {self.sensor!r}")
         c.egoradius = ego
         c.pad = self.pad
         c.mini_map_rad = mini
@@ -145,7 +147,7 @@ class BatchCoverageEnv:
         self.obs_shape = (self.num_agents, lay.obs_layers, lay.obs_side, lay.obs_side)
         self.num_actions = 4
 
-        if isinstance(self.sensor, LidarSensor):
+        if self.sensor.sensor_type == LidarSensor.sensor_type:
             self._upload_beams(self.sensor)
             self.sensor.add_listener(self._upload_beams)
 
@@ -199,7 +201,7 @@ class BatchCoverageEnv:
 
     def close(self):
         if getattr(self, "_h", None):
-            if isinstance(getattr(self, "sensor", None), LidarSensor):
+            if getattr(getattr(self, "sensor", None), "sensor_type", None) == LidarSensor.sensor_type:
                 self.sensor.remove_listener(self._upload_beams)
             self.lib.mc_destroy(self._h)
             self._h = None

@@ -229,27 +229,43 @@ __global__ __launch_bounds__(256) void sg_reset_kernel(SState s, const uint8_t* 
 }
 
 // --------------------------------------------------------------------------
-// SuperGridRL.step (:74-225), one wave per env, lane i = robot i.
+// SuperGridRL.step (:74-225).  GPW envs per wave: the wave's lanes form GPW
+// groups of NG = 64 / GPW lanes, lane li of group grp = robot li of env
+// (wave * GPW + grp) (N <= NG).  Cross-lane steps (occupancy ballots, robot
+// broadcasts, the count sum) stay inside a group; the few envs of a wave that
+// finish an episode are then reset one after another by the whole wave.
+// With N = 4, GPW = 16 fills every lane: one wave does what 16 did.
 // --------------------------------------------------------------------------
 // R >= 0: senseradius R at compile time — the window of every plane around
 // the PRE-move cell, extended by the one cell a move can shift it, is loaded
 // in a single round together with the target's dist value, and the post-move
 // window comes from registers (one load round instead of one per window row,
 // twice).  R < 0: any radius, rows loaded as the loops reach them.
-template <int R>
+template <int R, int GPW>
 __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* __restrict__ actions,
                                                       const int32_t* __restrict__ quot,
                                                       double* __restrict__ reward,
                                                       uint8_t* __restrict__ done) {
-  __shared__ double s_v[kEnvsPerBlock][kMaxAgents];
-  __shared__ int s_x[kEnvsPerBlock][kMaxAgents], s_y[kEnvsPerBlock][kMaxAgents];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int e = blockIdx.x * kEnvsPerBlock + w;
-  if (e >= s.B) return;
+  constexpr int NG = 64 / GPW;  // lanes per env
+  __shared__ double s_v[kEnvsPerBlock * GPW][NG];
+  __shared__ int s_x[kEnvsPerBlock * GPW][NG], s_y[kEnvsPerBlock * GPW][NG];
+  const int lane = threadIdx.x & 63;
+  const int grp = GPW == 1 ? 0 : lane / NG, li = GPW == 1 ? lane : lane & (NG - 1), gb = grp * NG;
+  const int slot_env = (threadIdx.x >> 6) * GPW + grp;  // env slot within the block
+  const int e_raw = blockIdx.x * (kEnvsPerBlock * GPW) + slot_env;
+  const bool valid = e_raw < s.B;
+  const int e = valid ? e_raw : s.B - 1;
+  // group-local ballot (bit j = lane li == j of this env) and broadcast
+  auto gballot = [&](bool p) -> uint64_t {
+    const uint64_t m = __ballot(p);
+    return GPW == 1 ? m : (m >> gb) & low_mask(NG);
+  };
+  auto gshfl = [&](int v, int z) -> int { return __shfl(v, gb + z); };
   const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = R >= 0 ? R : s.r;
-  const bool me = lane < N;
+  const bool me = valid && li < N;
   // every load that depends only on e is issued up front (one round trip)
-  const int my_act = me ? (int)actions[(size_t)e * N + lane] : 255;  // slot `lane`'s action byte
+  const int my_act = me ? (int)actions[(size_t)e * N + li] : 255;  // slot `li`'s action byte
+  const int act0 = (int)actions[(size_t)e * N];
   const int g = s.env_grid[e];
   const int q = quot ? quot[e] : 0;
   const int ap = s.a_prev[e];
@@ -257,10 +273,10 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
   const uint32_t cc0 = s.cov_cnt[e];
   const double dt = s.done_thresh[e];
   const int npos = s.numpos[g];
-  bool is_done;
-  if (__shfl(my_act, 0) == 255) {  // action == -1 / None (:88-90)
-    is_done = true;
-    if (lane == 0) {
+  int dn = 0;
+  if (act0 == 255) {  // action == -1 / None (:88-90); uniform over the group
+    dn = 1;
+    if (valid && li == 0) {
       reward[e] = 0.0;
       done[e] = 1;
       s.ep_pc[e] = (double)cc0 / (double)npos;
@@ -274,19 +290,19 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     uint64_t* obst = s.obst + (size_t)e * mw;
     int x = -(1 << 20), y = -(1 << 20);
     if (me) {
-      x = s.pos[((size_t)e * N + lane) * 2];
-      y = s.pos[((size_t)e * N + lane) * 2 + 1];
+      x = s.pos[((size_t)e * N + li) * 2];
+      y = s.pos[((size_t)e * N + li) * 2 + 1];
     }
     const int x_old = x, y_old = y;
-    // reward slot of robot `lane` (r2c): its rank by x + y*W with scanning
-    int slot = lane;
+    // reward slot of robot `li` (r2c): its rank by x + y*W with scanning
+    int slot = li;
     if (s.scan) {
       const int sc = x + y * W;
       int rank = 0;
-      for (int j = 0; j < N; ++j) rank += __shfl(sc, j) < sc;
+      for (int j = 0; j < N; ++j) rank += gshfl(sc, j) < sc;
       slot = rank;
     }
-    const int slot_act = __shfl(my_act, slot);
+    const int slot_act = gshfl(my_act, slot < NG ? slot : 0);
     const int u = me ? slot_act : 255;
     int tx = x, ty = y;
     if (u == 0) tx = x - 1;
@@ -322,13 +338,12 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     }
     double v = 0.0;
     for (int k = 0; k < N; ++k) {  // slot order; robot z = the one with slot k
-      const int z = s.scan ? (__ffsll((unsigned long long)__ballot(me && slot == k)) - 1) : k;
-      const int zu = __shfl(u, z);
-      if (zu >= 4) continue;  // not a move: nothing happens (no penalty)
-      const int zx = __shfl(tx, z), zy = __shfl(ty, z);
-      const int zok = __shfl((int)gfree, z);
-      const bool occ = __ballot(me && x == zx && y == zy) != 0ull;
-      if (lane == z) {
+      const int z = s.scan ? (__ffsll((unsigned long long)gballot(me && slot == k)) - 1) : k;
+      const int zu = gshfl(u, z);
+      const int zx = gshfl(tx, z), zy = gshfl(ty, z);
+      const int zok = gshfl((int)gfree, z);
+      const bool occ = gballot(me && x == zx && y == zy) != 0ull;
+      if (zu < 4 && li == z) {  // not a move: nothing happens (no penalty)
         if (zok && !occ) {
           x = zx;
           y = zy;
@@ -339,8 +354,8 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
       }
     }
     if (me) {
-      s_x[w][lane] = x;
-      s_y[w][lane] = y;
+      s_x[slot_env][li] = x;
+      s_y[slot_env][li] = y;
     }
     wave_sync();
 
@@ -371,10 +386,10 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
         const uint32_t fpos = field(xp, gpos, jj, j);
         const uint32_t fcov = field(xc, cov, jj, j);
         uint32_t lower = 0;
-        for (int m = 0; m < N; ++m) {  // uniform trip count; robots m < lane count
-          const int xm = s_x[w][m], ym = s_y[w][m];
+        for (int m = 0; m < N; ++m) {  // uniform trip count; robots m < li count
+          const int xm = s_x[slot_env][m], ym = s_y[slot_env][m];
           const uint32_t cm = mask32(max(0, ym - r - c0), min(n, ym + r + 1 - c0));
-          lower |= (m < lane && abs(j - xm) <= r) ? cm : 0u;
+          lower |= (m < li && abs(j - xm) <= r) ? cm : 0u;
         }
         const uint32_t ge0 = vm & ~fneg;
         const uint32_t nw = ge0 & ~fcov & ~lower;
@@ -429,27 +444,27 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     // the same step: that clear is skipped, so no store has to wait for
     // another (robots are distinct, so each cell gets one store at most)
     const bool moved = me && (x != x_old || y != y_old);
-    const size_t lay = (size_t)(s.scan ? 0 : lane) * WL;
+    const size_t lay = (size_t)(s.scan ? 0 : li) * WL;
     bool reoccupied = false;
-    if (s.scan)
-      for (int m = 0; m < N; ++m) reoccupied |= s_x[w][m] == x_old && s_y[w][m] == y_old;
+    if (s.scan && me)
+      for (int m = 0; m < N; ++m) reoccupied |= s_x[slot_env][m] == x_old && s_y[slot_env][m] == y_old;
     if (moved && !reoccupied) pl[lay + (size_t)x_old * L + y_old] = 0;
     if (moved) pl[lay + (size_t)x * L + y] = 1;
 
     // motion_penalty(a) on every slot (:203-208, 227-243): a is the quotient
     // left in `action` after the digit loop; a == inv(a) never holds
-    if ((q < 0 || q >= 4) && lane == 0) atomicOr(s.err, ERR_KEY);
+    if ((q < 0 || q >= 4) && valid && li == 0) atomicOr(s.err, ERR_KEY);
     v = v + ((q == ap) ? 0.0 : -1.0);
     if (me) {
-      s_v[w][slot] = v;
-      s.pos[((size_t)e * N + lane) * 2] = x;
-      s.pos[((size_t)e * N + lane) * 2 + 1] = y;
+      s_v[slot_env][slot] = v;
+      s.pos[((size_t)e * N + li) * 2] = x;
+      s.pos[((size_t)e * N + li) * 2 + 1] = y;
     }
-    cnt = wave_sum(cnt);
+#pragma unroll
+    for (int o = NG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);  // group sum
     wave_sync();
-    int dn = 0;
-    if (lane == 0) {
-      double total = np_pairwise_sum(s_v[w], N);
+    if (valid && li == 0) {
+      double total = np_pairwise_sum(s_v[slot_env], N);
       const int cs = cs0 + 1;
       const uint32_t cc = cc0 + (uint32_t)cnt;
       const double pc = (double)cc / (double)npos;
@@ -467,11 +482,17 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
         s.ep_len[e] = cs;
       }
     }
-    is_done = __shfl(dn, 0) != 0;
   }
-  if (is_done && s.auto_reset) {
+  // auto-reset: the wave's finished envs, one after another, each by every
+  // lane of the wave (sg_reset_env draws 64 candidates per round)
+  uint64_t rs = __ballot(s.auto_reset && valid && li == 0 && dn != 0);
+  if (rs) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the step's map ORs land first
-    sg_reset_env(s, e, lane, nullptr);
+    const int e0 = blockIdx.x * (kEnvsPerBlock * GPW) + (int)(threadIdx.x >> 6) * GPW;
+    for (; rs; rs &= rs - 1) {
+      const int gj = (__ffsll((unsigned long long)rs) - 1) / NG;
+      sg_reset_env(s, e0 + gj, lane, nullptr);
+    }
   }
 }
 
@@ -1093,19 +1114,38 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   hipStream_t st = (hipStream_t)stream;
   SG_TRY(hipSetDevice(E->device));
   if (E->stale) SG_TRY(launch_dist(E, st));  // the pre-move distance_map of the current maps
-  const int blocks = (E->s.B + mcs::kEnvsPerBlock - 1) / mcs::kEnvsPerBlock;
-  auto kern = mcs::sg_step_kernel<-1>;
-  switch (E->s.r) {  // compile-time radii of the reference configs (staged window)
-    case 1: kern = mcs::sg_step_kernel<1>; break;
-    case 2: kern = mcs::sg_step_kernel<2>; break;
-    case 3: kern = mcs::sg_step_kernel<3>; break;
-    default: break;
-  }
+  // envs per wave: as many groups of (N rounded up to a power of two) lanes
+  // as fit 64, capped by MARLCOV_SG_GPW (A/B: 1, 2, 4, 8, 16)
+  static const int gpw_cap = [] {
+    const char* v = getenv("MARLCOV_SG_GPW");
+    const int c = v ? atoi(v) : 16;
+    return c >= 1 ? c : 16;
+  }();
+  int gpw = 1;
+  while (gpw < 16 && 2 * gpw <= gpw_cap && E->s.N <= 64 / (2 * gpw)) gpw *= 2;
   static const bool force_generic = [] {  // MARLCOV_SG_GENERIC=1: A/B against the runtime-radius kernel
     const char* v = getenv("MARLCOV_SG_GENERIC");
     return v && atoi(v) == 1;
   }();
-  if (force_generic) kern = mcs::sg_step_kernel<-1>;
+  const int R = force_generic ? -1 : (E->s.r >= 1 && E->s.r <= 3 ? E->s.r : -1);
+  decltype(&mcs::sg_step_kernel<-1, 1>) kern = nullptr;
+#define SG_PICK(RR)                                                  \
+  switch (gpw) {                                                     \
+    case 1: kern = mcs::sg_step_kernel<RR, 1>; break;                \
+    case 2: kern = mcs::sg_step_kernel<RR, 2>; break;                \
+    case 4: kern = mcs::sg_step_kernel<RR, 4>; break;                \
+    case 8: kern = mcs::sg_step_kernel<RR, 8>; break;                \
+    default: kern = mcs::sg_step_kernel<RR, 16>; break;              \
+  }
+  switch (R) {  // compile-time radii of the reference configs (staged window)
+    case 1: SG_PICK(1); break;
+    case 2: SG_PICK(2); break;
+    case 3: SG_PICK(3); break;
+    default: SG_PICK(-1); break;
+  }
+#undef SG_PICK
+  const int per_block = mcs::kEnvsPerBlock * gpw;
+  const int blocks = (E->s.B + per_block - 1) / per_block;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * mcs::kEnvsPerBlock), 0, st, E->s, dev_actions, dev_quot,
                      dev_reward, dev_done);
   SG_TRY(hipGetLastError());
