@@ -75,7 +75,7 @@ struct Env {
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
   double* mini_obs = nullptr; // mini_map_rad: caller's float64 [B][N][2][E][E]
-  uint32_t* dist_list = nullptr;  // dist_reward: [B*N] maps for the full transform + count
+  uint32_t* dist_list = nullptr;  // dist_reward: count, workgroups done, last count + [B*N] maps (full transform)
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
@@ -109,7 +109,7 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_GRID_NEG: return {(void*)s.grid_neg, G * mw * 8};
     case MC_FIELD_GRID_POS: return {(void*)s.grid_pos, G * mw * 8};
     case MC_FIELD_DIST_MW: return {s.dist_mw, s.dist_mw ? B * N * 8 : -1};
-    case MC_FIELD_DIST_LISTED: return {E->dist_list, E->dist_list ? 4 : -1};
+    case MC_FIELD_DIST_LISTED: return {E->dist_list ? E->dist_list + 2 : nullptr, E->dist_list ? 4 : -1};
     case MC_FIELD_EP_PC: return {s.ep_pc, B * 8};
     case MC_FIELD_EP_LEN: return {s.ep_len, B * 4};
     case MC_FIELD_DJ_LISTED: return {E->dj_list ? E->dj_list + 2 : nullptr, E->dj_list ? 4 : -1};
@@ -389,7 +389,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     // work list of the full transform and its count
     void *mw = nullptr, *lq = nullptr;
     if (dev_alloc(E, &mw, (size_t)s.B * s.N * 8) != MC_OK ||
-        dev_alloc(E, &lq, ((size_t)s.B * s.N + 1) * 4) != MC_OK ||
+        dev_alloc(E, &lq, ((size_t)s.B * s.N + 3) * 4) != MC_OK ||
         hipMemset(mw, 0xFF, (size_t)s.B * s.N * 8) != hipSuccess) {
       std::string msg = g_err;
       mc_destroy(E);
@@ -639,7 +639,7 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
 static int dist_terms(Env* E, int post, hipStream_t st) {
   if (!E->cfg.dist_reward) return MC_OK;
   if (post)  // window search per map, full transform for the maps whose max(d) may have changed
-    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 1,
+    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 3,
                                  E->dist_list, st));
   else
     HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, 0, E->dist_pre, E->dist_obs, st));

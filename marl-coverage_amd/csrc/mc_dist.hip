@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                                                             float* __restrict__ pre_out,
                                                             float* __restrict__ dist_obs,
                                                             const uint32_t* __restrict__ list,
-                                                            const uint32_t* __restrict__ count) {
+                                                            uint32_t* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_cov;
   __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
   // of a device work list (a fixed grid strides over *count entries: the
   // count is uniform, so every wave reaches the end)
-  const uint32_t n_items = list ? *count : (uint32_t)gridDim.x;
+  const uint32_t n_items = list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x;
   for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
     const uint32_t ea = list ? list[it] : it;
     const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
@@ -336,6 +336,22 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
     __syncthreads();  // the LDS is reused by the next item
   }
+  // count[0] = entries, count[1] = workgroups done: the last workgroup to
+  // finish zeroes both for the next step's window search (every workgroup has
+  // read the entry count before it counts itself done; no memset launch per
+  // step) and keeps the entry count in count[2] (MC_FIELD_DIST_LISTED)
+  if (list && threadIdx.x == 0) {
+    uint32_t* cnt = count;
+    if (n_items == 0) {
+      if (blockIdx.x == 0) cnt[2] = 0;
+    } else {
+      __threadfence();
+      if (atomicAdd(cnt + 1, 1u) == gridDim.x - 1) {
+        atomicExch(cnt + 2, atomicExch(cnt, 0u));
+        atomicExch(cnt + 1, 0u);
+      }
+    }
+  }
 }
 
 size_t dist_lds_bytes(const State& s, int pad) {
@@ -346,7 +362,7 @@ int dist_max_rows() { return kMaxRows; }
 
 // the instantiation whose register chunk holds ceil(RX / kChunks) rows
 static hipError_t launch_full(const State& s, int pad, int post, float* pre_out, float* dist_obs,
-                              const uint32_t* list, const uint32_t* count, unsigned grid,
+                              const uint32_t* list, uint32_t* count, unsigned grid,
                               hipStream_t stream) {
   const int RX = s.Wp + 2 * pad, cl = chunk_rows(RX);
   const size_t lds = dist_lds_bytes(s, pad);
@@ -466,11 +482,9 @@ __global__ __launch_bounds__(kLocalThreads) void dist_local_kernel(State s, int 
 hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
                             uint32_t* list, uint32_t* count, hipStream_t stream) {
   const size_t maps = (size_t)s.B * s.N;
-  hipError_t err = hipMemsetAsync(count, 0, 4, stream);
-  if (err != hipSuccess) return err;
   hipLaunchKernelGGL(dist_local_kernel, dim3((unsigned)((maps * kWin + kLocalThreads - 1) / kLocalThreads)),
                      dim3(kLocalThreads), 0, stream, s, pad, pre_out, dist_obs, list, count);
-  err = hipGetLastError();
+  hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
   return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, stream);

@@ -1115,11 +1115,13 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   SG_TRY(hipSetDevice(E->device));
   if (E->stale) SG_TRY(launch_dist(E, st));  // the pre-move distance_map of the current maps
   // envs per wave: as many groups of (N rounded up to a power of two) lanes
-  // as fit 64, capped by MARLCOV_SG_GPW (A/B: 1, 2, 4, 8, 16)
+  // as fit 64, capped at 4 (MARLCOV_SG_GPW overrides the cap).  sg_c2
+  // (tools/gpu_sg_gpw.sh, rocprof): 1 19.7 us, 2 15.7, 4 14.7, 8 15.3, 16 17.8
+  // -- past 4 envs per wave there are too few waves to hide the window loads
   static const int gpw_cap = [] {
     const char* v = getenv("MARLCOV_SG_GPW");
-    const int c = v ? atoi(v) : 16;
-    return c >= 1 ? c : 16;
+    const int c = v ? atoi(v) : 4;
+    return c >= 1 ? c : 4;
   }();
   int gpw = 1;
   while (gpw < 16 && 2 * gpw <= gpw_cap && E->s.N <= 64 / (2 * gpw)) gpw *= 2;

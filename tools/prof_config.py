@@ -113,8 +113,8 @@ def main():
             counters.setdefault(k, {}).setdefault(d, lst)
     step = collections.defaultdict(float)
     for k, durs in tr.items():
-        if len(durs) < K:
-            continue  # not a per-step kernel (setup, grid generation, resets)
+        if len(durs) < K or "random_actions" in k:
+            continue  # not a per-step kernel of the timed region (setup, grids, resets, action staging)
         timed = durs[-K:]
         ent = {"dispatches_total": len(durs), "timed_dispatches": K,
                "mean_us": round(statistics.mean(timed), 3), "median_us": round(statistics.median(timed), 3)}

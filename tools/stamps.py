@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--config", default="c2")
     ap.add_argument("--build-only", action="store_true")
     args = ap.parse_args()
     if args.build_only or not os.path.exists(LIB):
@@ -42,16 +43,18 @@ def main():
     from marlcov import _lib
     import bench
 
-    c = bench.CONFIGS["c2"]
-    cfg = dict(bench.BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"])
+    c = bench.CONFIGS[args.config]
+    cfg = dict(bench.BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
+               **c.get("extra", {}))
     B = args.envs
-    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=128, length=128, prob_obst=0.1, seed=1000),
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1, seed=1000),
                                    seed=1, auto_reset=True)
+    print("kernel:", env.kernel_variant())
     st = torch.zeros((B, 16), dtype=torch.int64, device=env.device)
     _lib.check(env.lib.mc_debug_stamps(env._h, st.data_ptr()), "stamps")
     env.reset()
     for t in range(args.steps):
-        a = torch.randint(0, 4, (B, 4), dtype=torch.uint8, device=env.device)
+        a = torch.randint(0, 4, (B, env.num_agents), dtype=torch.uint8, device=env.device)
         env.step(a)
     torch.cuda.synchronize()
     s = st.cpu().numpy().astype(np.int64)
@@ -60,7 +63,7 @@ def main():
     print(f"envs={B}  wave start spread (cycles): median {np.median(s[:,0]-t0):.0f}  max {(s[:,0]-t0).max()}")
     print(f"kernel span (first start -> last end): {s[:,10].max()-t0} cycles")
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    acts = torch.randint(0, 4, (20, B, 4), dtype=torch.uint8, device=env.device)
+    acts = torch.randint(0, 4, (20, B, env.num_agents), dtype=torch.uint8, device=env.device)
     ev0.record()
     for t in range(20):
         env.step(acts[t])
