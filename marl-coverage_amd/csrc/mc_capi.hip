@@ -490,8 +490,12 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     // the pattern of most starts; it stands for the beam's table when every
     // start a robot can occupy (1 .. cm-2: the border is -1) visits the same
     // cells with it up to the first border cell of the minor axis, where the
-    // march ends (an obstacle) -- then the rest of the word is never read
+    // march ends (an obstacle) -- then the rest of the word is never read.
+    // A beam without such a pattern is flagged (axis bit 1) and marches from
+    // its per-start table (C4's 360 beams: 2 of them, 270 and 315 degrees,
+    // whose float64 chains truncate differently at starts 1..3)
     {
+      bool bc = true;
       const uint64_t* row = &bits[(size_t)b * cmax];
       uint64_t best = row[cm > 2 ? 1 : 0];
       int best_n = 0;
@@ -502,15 +506,17 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
         if (2 * n > cm) break;
       }
       o.bits = (uint32_t)best;
-      for (int c0 = 1; c0 + 1 < cm && common; ++c0) {
+      for (int c0 = 1; c0 + 1 < cm && bc; ++c0) {
         int a = c0, c = c0;  // cell of the start's own word / of the common word
         for (int k = 0; k < K; ++k) {
           a += ((row[c0] >> k) & 1) ? o.msign : 0;
           c += ((best >> k) & 1) ? o.msign : 0;
-          if (a != c) { common = false; break; }
+          if (a != c) { bc = false; break; }
           if (a <= 0 || a >= cm - 1) break;  // border reached: the march ends here
         }
       }
+      if (!bc) o.axis |= 2;
+      common = common && bc;
     }
   }
   HIP_TRY(hipSetDevice(E->device));
@@ -547,7 +553,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     const mc::Beam& o = bt[b];
     if (o.K < 1) continue;
     const int mv = (o.bits & 1u) ? o.msign : 0;
-    const int dx = o.axis == 0 ? o.sign : mv, dy = o.axis == 0 ? mv : o.sign;
+    const int dx = (o.axis & 1) == 0 ? o.sign : mv, dy = (o.axis & 1) == 0 ? mv : o.sign;
     k1 |= 1u << (3 * (dx + 1) + (dy + 1));
   }
   E->s.beam_k1 = E->s.beam_common && !getenv("MARLCOV_NO_K1") ? k1 : 0u;

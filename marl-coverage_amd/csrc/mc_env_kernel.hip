@@ -661,13 +661,15 @@ __device__ __forceinline__ Ray ray_init(const State& s, const Lds<WT>& L, int id
   // itself (no per-step base add)
   const uint32_t plane = (uint32_t)(uintptr_t)(const lds_char*)(const char*)L.negr;
   R.P = ((plane + (uint32_t)row * (uint32_t)sizeof(WT)) << 6) | (uint32_t)col;
-  const bool ax = bm.axis == 0;
+  const bool ax = (bm.axis & 1) == 0;
   R.d0 = (uint32_t)(ax ? bm.sign * RB : bm.sign);
   R.d1 = (uint32_t)(ax ? bm.msign : bm.msign * RB);
   R.K = R.live ? bm.K : -1;
+  // the beam's own step bits unless its pattern depends on the start
+  // coordinate (Beam::axis bit 1: mc_set_beam_table; C4: 2 of 360 beams)
   R.bits = !R.live ? 0u
-           : s.beam_common ? bm.bits
-                           : (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)];
+           : (s.beam_common || !(bm.axis & 2)) ? bm.bits
+                                               : (uint32_t)s.beam_bits[(size_t)b * s.bcmax + (ax ? ya : xa)];
   return R;
 }
 
@@ -864,9 +866,12 @@ __device__ __forceinline__ void single_tool(const State& s, const Ctx<NT, EPW, W
 // every block that holds it.  Also folds the marks into the old tiles (the
 // obs crops read the post-step maps).
 // --------------------------------------------------------------------------
+// marks_in_regs: the lidar's free marks are in I.mf (else L.fp: the square
+// sensor, or single_square_tool's own cell); obst_in_regs: its obstacle marks
+// are in I.mo (lidar, with or without single_square_tool; else L.op)
 template <int NT, int EPW, typename WT, int KI, int NS>
 __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I,
-                                      bool marks_in_regs) {
+                                      bool marks_in_regs, bool obst_in_regs) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   const Lds<WT>& L = C.L;
   const int TW = s.TW;
@@ -893,7 +898,7 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
     I.nf[k] = I.no[k] = I.nu[k] = 0;
     if (idx < items) {
       const uint64_t fp = marks_in_regs ? I.mf[k] : L.fp[idx];
-      const uint64_t op = marks_in_regs ? I.mo[k] : L.op[idx];
+      const uint64_t op = obst_in_regs ? I.mo[k] : L.op[idx];
       uint64_t f0, o0, u0;
       old_tiles<KI>(I, k, f0, o0, u0);  // first use of the mask loads
       I.f[k] = f0;
@@ -994,7 +999,7 @@ __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EP
     single_tool<NT, EPW, WT>(s, C);
     __syncthreads();
   }
-  merge<NT, EPW, WT, KI, NS>(s, C, I, s.sensor == 0 && !s.sst);
+  merge<NT, EPW, WT, KI, NS>(s, C, I, s.sensor == 0 && !s.sst, s.sensor == 0);
 }
 
 // --------------------------------------------------------------------------
@@ -1428,8 +1433,13 @@ __global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uin
     // (the same loop on the scalar unit, robots read by v_readlane, was
     // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
     if constexpr (!FRONT) {  // (FRONT: moved during round trip 2)
-      if constexpr (SH::N > 0 && SH::N <= 8) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
-      else if (C.sub < 64) moves<NT, EPW, WT>(s, C, -s.pen);
+      // the first wave of the slot moves the robots (lane 0 publishes); the
+      // other waves of a multi-wave workgroup only wait at the barrier
+      if constexpr (SH::N > 0 && SH::N <= 8) {
+        if (NT == 64 || C.sub < 64) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
+      } else if (C.sub < 64) {
+        moves<NT, EPW, WT>(s, C, -s.pen);
+      }
       __syncthreads();
     }
     STAMP(3);

@@ -28,10 +28,11 @@ enum : uint32_t {
 // visits cells k = 0..K unless an obstacle stops it.
 struct Beam {
   int32_t K;
-  int16_t axis;   // 0: major axis is x (rows), 1: major axis is y (columns)
+  int16_t axis;   // bit 0 -- 0: major axis is x (rows), 1: y (columns); bit 1: march
+                  // from the per-start table (no common pattern for this beam)
   int16_t sign;   // +1 / -1 along the major axis
   int32_t msign;  // +1 / -1 / 0: direction of a minor-axis move
-  uint32_t bits;  // the step bits shared by every start (State::beam_common)
+  uint32_t bits;  // the step bits shared by every start (unless axis bit 1)
 };
 static_assert(sizeof(Beam) == 16, "Beam is 16 bytes");
 

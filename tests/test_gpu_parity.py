@@ -89,6 +89,13 @@ BATCH_CASES = {
     "single_square_tool": (base_cfg(numrobot=2, single_square_tool=1, sensor_type="square_sensor",
                                     sensor_config={"range": 2}),
                            lambda rs: bern(rs, 30, 30, 0.2), 8, 30),
+    # single_square_tool with the lidar: the free map gets only the robot's
+    # cell, the obstacle map the lidar's marks (dec_grid_rl.py:232-236)
+    "lidar_single_tool": (base_cfg(numrobot=3, single_square_tool=1, sensor_config={"num_lasers": 13, "range": 5}),
+                          lambda rs: bern(rs, 30, 30, 0.2), 8, 30),
+    "lidar360_single_tool": (base_cfg(numrobot=2, single_square_tool=1, allow_even_beams=True,
+                                      sensor_config={"num_lasers": 360, "range": 8}),
+                             lambda rs: bern(rs, 40, 40, 0.15), 4, 20),
     "map_sharing_comm": (base_cfg(numrobot=4, comm_radius=7, allow_comm=1, map_sharing=1,
                                   sensor_config={"num_lasers": 15, "range": 5}),
                          lambda rs: bern(rs, 40, 40, 0.15), 8, 30),
