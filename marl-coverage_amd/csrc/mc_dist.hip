@@ -50,6 +50,13 @@ namespace {
 constexpr int kDtThreads = 512;
 constexpr int kStrip = 32;                     // columns per strip
 constexpr int kChunks = kDtThreads / kStrip;   // row chunks per column in the column pass
+// LDS strides, padded off the bank period: a strip row is 36 u16 (72 B = 18
+// dwords: the row pass's 8-byte stores of 16 consecutive rows hit 32
+// distinct banks; at 64 B four rows shared each bank), a column's chunk
+// minima 20 u32 (the column pass's 16-byte reads of 16 columns hit distinct
+// banks; at 16 u32 four columns shared them)
+constexpr int kSP = 36;
+constexpr int kCM = 20;
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
 constexpr int kRowOff = 1024;                  // min(g - u) + kRowOff >= 0 (u < kMaxRows)
@@ -70,9 +77,9 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   DtLds L;
   const int RW = (RY + 63) >> 6;
   L.cb = (size_t)RX * RW * 8;
-  const size_t st = (size_t)kChunks * chunk_rows(RX) * kStrip * 2, tiles = (size_t)MT * 8;
+  const size_t st = (size_t)kChunks * chunk_rows(RX) * kSP * 2, tiles = (size_t)MT * 8;
   L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
-  L.mins = (size_t)2 * kChunks * kStrip * 4;
+  L.mins = (size_t)2 * kStrip * kCM * 4;
   L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
   L.total = L.cb + L.strip + L.mins + L.tgt;
   return L;
@@ -93,9 +100,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   const int T = post ? 5 + E * E : 5;
   const DtLds LL = dt_lds(RX, RY, s.MT, 5 + E * E);
   uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
-  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kStrip]
+  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kSP] (kStrip used)
   constexpr int RXP = kChunks * kCL;                         // strip rows incl. padding
-  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [2][kStrip][kChunks]
+  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [2][kStrip][kCM] (kChunks used)
   int* s_d = reinterpret_cast<int*>(smem + LL.cb + LL.strip + LL.mins);
   const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
@@ -165,10 +172,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       for (int q = 0; q < 2; ++q) {
         const int u = tid + q * kDtThreads;
         if (u >= RXP) continue;
-        uint4* grow = reinterpret_cast<uint4*>(G + u * kStrip);
+        uint2* grow = reinterpret_cast<uint2*>(G + u * kSP);
         if (u >= RX) {  // padding rows: no covered cell
 #pragma unroll
-          for (int k = 0; k < 4; ++k) grow[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+          for (int k = 0; k < 8; ++k) grow[k] = make_uint2(~0u, ~0u);
           continue;
         }
         const uint64_t cw = Cb[u * RW + w];
@@ -222,8 +229,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
         if (sb == ~0u) lastL[q] = c0 + 31;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          grow[k] = make_uint4(pk[4 * k], pk[4 * k + 1], pk[4 * k + 2], pk[4 * k + 3]);
+        for (int k = 0; k < 8; ++k) grow[k] = make_uint2(pk[2 * k], pk[2 * k + 1]);
       }
       __syncthreads();
       // ---- column pass: this thread's chunk of column c0 + col into registers.
@@ -233,21 +239,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       asm volatile("" : "+v"(u0));
       int gv[kCL];
       int pmin = kInf, smin = kInf;
-      uint16_t* gcol = G + u0 * kStrip + col;  // row u0 + i at gcol[i * kStrip]
+      uint16_t* gcol = G + u0 * kSP + col;  // row u0 + i at gcol[i * kSP]
 #pragma unroll
       for (int i = 0; i < kCL; ++i) {
-        gv[i] = (int)gcol[i * kStrip];
+        gv[i] = (int)gcol[i * kSP];
         pmin = min(pmin, gv[i] - (u0 + i));
         smin = min(smin, gv[i] + (u0 + i));
       }
       // chunk minima, packed: low half min(g - u) + RXOFF, high half min(g + u)
-      uint32_t* cmin = s_cmin + (st & 1) * (kChunks * kStrip);  // double buffer: 2 barriers per strip
-      cmin[col * kChunks + chunk] =
+      uint32_t* cmin = s_cmin + (st & 1) * (kStrip * kCM);  // double buffer: 2 barriers per strip
+      cmin[col * kCM + chunk] =
           (uint32_t)min(pmin + kRowOff, 0xFFFF) | ((uint32_t)min(smin, 0xFFFF) << 16);
       __syncthreads();
       u16x2 accP = {0xFFFF, 0xFFFF}, accS = {0xFFFF, 0xFFFF};
       {
-        const uint4* cm = reinterpret_cast<const uint4*>(cmin + col * kChunks);
+        const uint4* cm = reinterpret_cast<const uint4*>(cmin + col * kCM);
 #pragma unroll
         for (int k = 0; k < kChunks / 4; ++k) {
           const uint4 q4 = cm[k];
