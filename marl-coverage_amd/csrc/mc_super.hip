@@ -263,16 +263,26 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
   auto gshfl = [&](int v, int z) -> int { return __shfl(v, gb + z); };
   const int N = s.N, W = s.W, L = s.L, RW = s.RW, r = R >= 0 ? R : s.r;
   const bool me = valid && li < N;
-  // every load that depends only on e is issued up front (one round trip)
-  const int my_act = me ? (int)actions[(size_t)e * N + li] : 255;  // slot `li`'s action byte
-  const int act0 = (int)actions[(size_t)e * N];
+  // every load that depends only on e is issued up front, unconditionally
+  // (clamped indices: lanes without a robot read robot 0; absent quotients
+  // read a_prev), and nothing is used before the one wait below, so the
+  // compiler cannot split the round (it sank the cell load behind a wait on
+  // the sentinel byte, and that behind the grid index)
+  const size_t ri = (size_t)e * N + (li < N ? li : 0);
+  const int2 p_raw = reinterpret_cast<const int2*>(s.pos)[ri];
+  const int act_raw = actions[ri];
+  const int act0 = actions[(size_t)e * N];
   const int g = s.env_grid[e];
-  const int q = quot ? quot[e] : 0;
+  const int q_raw = (quot ? quot : s.a_prev)[e];
   const int ap = s.a_prev[e];
   const int cs0 = s.currstep[e];
   const uint32_t cc0 = s.cov_cnt[e];
   const double dt = s.done_thresh[e];
-  const int npos = s.numpos[g];
+  asm volatile("" ::"v"(p_raw.x), "v"(p_raw.y), "v"(act_raw), "v"(act0), "v"(g), "v"(q_raw), "v"(ap),
+               "v"(cs0), "v"(cc0), "v"(dt));
+  const int my_act = me ? act_raw : 255;  // slot `li`'s action byte
+  const int q = quot ? q_raw : 0;
+  const int npos = s.numpos[g];  // used at the end only
   int dn = 0;
   if (act0 == 255) {  // action == -1 / None (:88-90); uniform over the group
     dn = 1;
@@ -288,11 +298,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     const uint64_t* gpos = s.gpos + (size_t)g * mw;
     uint64_t* cov = s.cov + (size_t)e * mw;
     uint64_t* obst = s.obst + (size_t)e * mw;
-    int x = -(1 << 20), y = -(1 << 20);
-    if (me) {
-      x = s.pos[((size_t)e * N + li) * 2];
-      y = s.pos[((size_t)e * N + li) * 2 + 1];
-    }
+    int x = me ? p_raw.x : -(1 << 20), y = me ? p_raw.y : -(1 << 20);
     const int x_old = x, y_old = y;
     // reward slot of robot `li` (r2c): its rank by x + y*W with scanning
     int slot = li;
@@ -312,23 +318,51 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     const bool inb = me && tx >= 0 && tx < W && ty >= 0 && ty < L;
     // pre-move distance_map[x, y] (:117-118, 139): the dist layer of the last
     // state (loaded whether or not the move succeeds: no wait on the grid)
-    double dv = 0.0;
-    if (s.dist && inb && u < 4) dv = (double)s.dist_plane[((size_t)e * W + tx) * L + ty];
+    // (unconditional, clamped cell, any valid plane without dist_reward: it
+    // joins the window's round)
+    const float* dpl = s.dist ? s.dist_plane : reinterpret_cast<const float*>(s.gneg);
+    const float dvr = dpl[s.dist && inb ? ((size_t)e * W + tx) * L + ty : 0];
     constexpr int NE = R >= 0 ? 2 * R + 3 : 1;  // extended window rows
     constexpr int kRowUnroll = R >= 0 ? 2 * R + 1 : 1;
     constexpr int kColUnroll = R >= 0 ? 2 * R + 1 : 1;
     uint32_t xn[NE], xp[NE], xc[NE];             // bit b = cell y - R - 1 + b
     bool gfree;
     if constexpr (R >= 0) {
+      // every window word is loaded unconditionally from a clamped address
+      // and masked afterwards: one round for all 6 * NE loads (predicated
+      // loads made the compiler wait after every row: NE round trips)
       const int c0e = y - R - 1;
+      const int w0 = c0e >> 6, sh = c0e & 63;  // arithmetic shift: floor
+      const bool wa = w0 >= 0 && w0 < RW, wb = w0 + 1 >= 0 && w0 + 1 < RW;
+      const size_t ia = wa ? (size_t)w0 : 0, ib = wb ? (size_t)(w0 + 1) : 0;
+      // (the field's low 32 bits need only the low dword of the second word)
+      uint64_t na[NE], pa[NE], ca[NE];
+      uint32_t nb[NE], pb[NE], cb[NE];
+      bool okr[NE];
+      auto lo32 = [](const uint64_t* p) -> uint32_t { return *reinterpret_cast<const uint32_t*>(p); };
 #pragma unroll
       for (int k = 0; k < NE; ++k) {
         const int j = x - R - 1 + k;
-        const bool ok = me && j >= 0 && j < W;
-        const size_t ro = (size_t)(ok ? j : 0) * RW;
-        xn[k] = ok ? row_field(gneg + ro, RW, c0e) : 0u;
-        xp[k] = ok ? row_field(gpos + ro, RW, c0e) : 0u;
-        xc[k] = ok ? row_field(cov + ro, RW, c0e) : 0u;
+        okr[k] = me && j >= 0 && j < W;
+        const size_t ro = (size_t)(okr[k] ? j : 0) * RW;
+        na[k] = gneg[ro + ia];
+        nb[k] = lo32(gneg + ro + ib);
+        pa[k] = gpos[ro + ia];
+        pb[k] = lo32(gpos + ro + ib);
+        ca[k] = cov[ro + ia];
+        cb[k] = lo32(cov + ro + ib);
+      }
+      auto fld = [&](uint64_t a, uint32_t b, bool ok) -> uint32_t {
+        const uint64_t A = (ok && wa) ? a : 0ull, Bw = (ok && wb) ? (uint64_t)b : 0ull;
+        return (uint32_t)(sh ? (A >> sh) | (Bw << (64 - sh)) : A);
+      };
+      asm volatile("" ::"v"(na[NE - 1]), "v"(nb[NE - 1]), "v"(pa[NE - 1]), "v"(pb[NE - 1]), "v"(ca[NE - 1]),
+                   "v"(cb[NE - 1]), "v"(dvr));  // the round's single wait
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        xn[k] = fld(na[k], nb[k], okr[k]);
+        xp[k] = fld(pa[k], pb[k], okr[k]);
+        xc[k] = fld(ca[k], cb[k], okr[k]);
       }
       const int ddx = tx - x, ddy = ty - y;
       const uint32_t trow = ddx < 0 ? xn[R] : (ddx > 0 ? xn[R + 2] : xn[R + 1]);
@@ -336,6 +370,7 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
     } else {
       gfree = inb && !bit_at(gneg, RW, tx, ty);
     }
+    const double dv = (s.dist && inb && u < 4) ? (double)dvr : 0.0;
     double v = 0.0;
     for (int k = 0; k < N; ++k) {  // slot order; robot z = the one with slot k
       const int z = s.scan ? (__ffsll((unsigned long long)gballot(me && slot == k)) - 1) : k;
