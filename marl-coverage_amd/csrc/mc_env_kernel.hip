@@ -88,13 +88,16 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   const int tiles = s.N * s.TW * s.TW;
   const int rows = row_plane_words(s.N, s.TW, (int)sizeof(WT));
   uint64_t* p = reinterpret_cast<uint64_t*>(smem);
-  L.neg = p;
-  L.pos = p + tiles;
-  L.fold = p + 2 * tiles;
-  L.oold = p + 3 * tiles;
-  L.fp = p + 4 * tiles;
-  L.op = p + 5 * tiles;
-  char* q = smem + (size_t)6 * tiles * 8;
+  // the grid tile planes (neg, pos) and the obstacle-mark plane (op) serve
+  // the square sensor only: a lidar slot carves fold, oold, fp (env_lds_bytes)
+  const bool square = s.sensor != 0;
+  L.fold = p;
+  L.oold = p + tiles;
+  L.fp = p + 2 * tiles;
+  L.neg = square ? p + 3 * tiles : nullptr;
+  L.pos = square ? p + 4 * tiles : nullptr;
+  L.op = square ? p + 5 * tiles : nullptr;
+  char* q = smem + (size_t)(square ? 6 : 3) * tiles * 8;
   L.negr = reinterpret_cast<WT*>(q);
   L.fpr = L.negr + rows;
   L.fldr = L.fpr + rows;
@@ -1302,8 +1305,19 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
 // --------------------------------------------------------------------------
 // the env kernel: EPW envs per workgroup
 // --------------------------------------------------------------------------
+// minimum waves per SIMD the compiler must leave room for (VGPR budget):
+// one env per 4-wave workgroup at C4, LDS-bound at 5 workgroups per CU
+template <int NT, class SH>
+constexpr int env_min_waves() {
+#ifdef MC_C4_WPE
+  return (NT == 256 && SH::NB == 360) ? MC_C4_WPE : 1;
+#else
+  return 1;
+#endif
+}
+
 template <int NT, int EPW, typename WT, class SH>
-__global__ __launch_bounds__(NT) void env_kernel(State s_in, int mode, const uint8_t* __restrict__ actions,
+__global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(State s_in, int mode, const uint8_t* __restrict__ actions,
                                                  const uint8_t* __restrict__ env_mask,
                                                  const int32_t* __restrict__ inj_pos,
                                                  double* __restrict__ reward_out,

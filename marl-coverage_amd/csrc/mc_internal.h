@@ -148,7 +148,8 @@ __host__ __device__ inline int row_plane_words(int N, int TW, int rowbytes) {
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
 // rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
 __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes) {
-  size_t b = (size_t)6 * N * TW * TW * 8;              // neg, pos, fold, oold, fp, op tiles
+  // fold, oold, fp tiles; the square sensor (nbeams == 0) also neg, pos, op
+  size_t b = (size_t)(nbeams > 0 ? 3 : 6) * N * TW * TW * 8;
   b += (((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
   b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
   b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
