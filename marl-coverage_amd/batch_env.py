@@ -288,10 +288,19 @@ class BatchCoverageEnv:
             _lib.FIELD_EP_PC: (B,), _lib.FIELD_EP_LEN: (B,), _lib.FIELD_DJ_LISTED: (1,),
         }[field]
 
-    def get_state(self, field):
+    def get_state(self, field, out=None):
+        """Device copy of one state field (`out`: a device tensor of the field's
+        shape and dtype to fill instead of a new one)."""
         torch = self._torch
-        t = torch.empty(self.field_shape(field), dtype=getattr(torch, _FIELD_DTYPES[field]),
-                        device=self.device)
+        if out is None:
+            t = torch.empty(self.field_shape(field), dtype=getattr(torch, _FIELD_DTYPES[field]),
+                            device=self.device)
+        else:
+            t = out
+            if (tuple(t.shape) != self.field_shape(field) or t.dtype != getattr(torch, _FIELD_DTYPES[field])
+                    or t.device != torch.device(self.device) or not t.is_contiguous()):
+                raise ValueError(f"out for field {field} must be a contiguous {_FIELD_DTYPES[field]} "
+                                 f"tensor of shape {self.field_shape(field)} on {self.device}")
         nbytes = t.numel() * t.element_size()
         _lib.check(self.lib.mc_get_state(self._h, field, t.data_ptr(), nbytes, self._stream()),
                    "mc_get_state")

@@ -195,10 +195,18 @@ class DecGridRL:
         env = self._env
         codes = decode_action(action, self._numrobot)
         sentinel = codes is None
-        a = np.full((1, self._numrobot), _lib.ACT_SENTINEL if sentinel else 0, dtype=np.uint8)
-        if not sentinel:
-            a[0] = codes
-        env.step(self._torch.from_numpy(a).to(env.device))
+        # the action row goes through a cached pinned buffer (asynchronous
+        # copy, ordered before the step on the stream)
+        torch = self._torch
+        ab = self.__dict__.get("_act_buf")
+        if ab is None or ab[0].shape[1] != self._numrobot or ab[1].device != torch.device(env.device):
+            ab = self._act_buf = (torch.empty((1, self._numrobot), dtype=torch.uint8, pin_memory=True),
+                                  torch.empty((1, self._numrobot), dtype=torch.uint8, device=env.device))
+        host, dev = ab
+        h = host.numpy()
+        h[0] = _lib.ACT_SENTINEL if sentinel else codes
+        dev.copy_(host, non_blocking=True)
+        env.step(dev)
         self._refresh(reset=False)
         if sentinel:
             reward, done = 0, True
@@ -210,31 +218,70 @@ class DecGridRL:
             return [obs, self._adjacency_matrix], reward, done
         return obs, reward, done
 
+    def _fetch(self, tensors):
+        """Device tensors -> NumPy arrays with ONE stream synchronization: each
+        is copied asynchronously into a cached pinned host buffer on the env's
+        stream (ordered after the step), then the stream is synchronized once
+        (the per-field ``.cpu()`` / ``.item()`` calls were one blocking copy
+        each: 160 -> 122 us per facade step, tools/facade_probe.py)."""
+        torch = self._torch
+        cache = self.__dict__.setdefault("_pinned", {})
+        out = []
+        for i, t in enumerate(tensors):
+            key = (i, tuple(t.shape), t.dtype)
+            h = cache.get(key)
+            if h is None:
+                h = cache[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
+            h.copy_(t, non_blocking=t.is_cuda)
+            out.append(h)
+        if any(t.is_cuda for t in tensors):
+            torch.cuda.current_stream(self._env.device).synchronize()
+        return [h.numpy() for h in out]
+
     def _refresh(self, reset):
         env = self._env
-        torch = self._torch
-        obs = env.obs[0].to("cpu", non_blocking=False)
-        self._obs_np = obs.numpy().astype(np.float64)
-        if env.dist_obs is not None and not self._dijkstra_input:
+        bufs = self.__dict__.get("_state_bufs")
+        if bufs is None or bufs[0] is not env:
+            torch = self._torch
+            bufs = self._state_bufs = (env, {f: torch.empty(env.field_shape(f), dtype=getattr(torch, d),
+                                                            device=env.device)
+                                             for f, d in ((_lib.FIELD_POS, "int32"),
+                                                          (_lib.FIELD_CURRSTEP, "int32"),
+                                                          (_lib.FIELD_DONE_THRESH, "float64"))})
+        sb = bufs[1]
+        pieces = [env.obs[0], env.get_state(_lib.FIELD_POS, out=sb[_lib.FIELD_POS])[0],
+                  env.get_state(_lib.FIELD_CURRSTEP, out=sb[_lib.FIELD_CURRSTEP])[:1],
+                  env.get_state(_lib.FIELD_DONE_THRESH, out=sb[_lib.FIELD_DONE_THRESH])[:1],
+                  env.reward[:1], env.done[:1]]
+        dist = env.dist_obs is not None and not self._dijkstra_input
+        if dist:
+            pieces.append(env.dist_obs[0])
+        if env.minimap_obs is not None:
+            pieces.append(env.minimap_obs[0])
+        if env.adj is not None:
+            pieces.append(env.adj[0])
+        got = self._fetch(pieces)
+        obs, pos, cs, dt, rew, dn = got[:6]
+        rest = got[6:]
+        self._obs_np = obs.astype(np.float64)
+        if dist:
             # float distance layer (the dijkstra path overwrites it, :354-358)
-            self._obs_np[:, 3] = env.dist_obs[0].cpu().numpy().astype(np.float64)
+            self._obs_np[:, 3] = rest.pop(0).astype(np.float64)
         if env.minimap_obs is not None:  # overwrites layers 3 and 4 (:365-370)
-            self._obs_np[:, 3:5] = env.minimap_obs[0].cpu().numpy()
-        pos = env.get_state(_lib.FIELD_POS)[0].cpu().numpy()
+            self._obs_np[:, 3:5] = rest.pop(0)
         self._xinds = pos[:, 0].astype(int)
         self._yinds = pos[:, 1].astype(int)
-        self._adjacency_matrix = env.adj[0].cpu().numpy().astype(np.float64)
-        self._currstep = int(env.get_state(_lib.FIELD_CURRSTEP)[0].item())
-        dt = float(env.get_state(_lib.FIELD_DONE_THRESH)[0].item())
-        if dt != float(self._dt):
-            self._dt = dt
+        if env.adj is not None:
+            self._adjacency_matrix = rest.pop(0).astype(np.float64)
+        self._currstep = int(cs[0])
+        if float(dt[0]) != float(self._dt):
+            self._dt = float(dt[0])
         if not reset:
-            self._reward_dev = float(env.reward[0].item())
-            self._done_dev = int(env.done[0].item())
+            self._reward_dev = float(rew[0])
+            self._done_dev = int(dn[0])
         rp = np.zeros(self._grid.shape)
         rp[self._xinds, self._yinds] = 1
         self._robot_pos_map = rp
-        del torch
 
     def get_egocentric_observations(self):
         return self._obs_np.copy()
