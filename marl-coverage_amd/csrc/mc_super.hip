@@ -1151,7 +1151,7 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   if (E->stale) SG_TRY(launch_dist(E, st));  // the pre-move distance_map of the current maps
   // envs per wave: as many groups of (N rounded up to a power of two) lanes
   // as fit 64, capped at 4 (MARLCOV_SG_GPW overrides the cap).  sg_c2
-  // (tools/gpu_sg_gpw.sh, rocprof): 1 19.7 us, 2 15.7, 4 14.7, 8 15.3, 16 17.8
+  // (tools/gpu_sg_gpw.sh, rocprof): 1 17.8 us, 2 14.3, 4 12.8, 8 14.6, 16 19.4
   // -- past 4 envs per wave there are too few waves to hide the window loads
   static const int gpw_cap = [] {
     const char* v = getenv("MARLCOV_SG_GPW");
