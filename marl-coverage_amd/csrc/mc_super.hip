@@ -532,6 +532,293 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
 }
 
 // --------------------------------------------------------------------------
+// SuperGridRL.step with each robot's window rows spread over lanes (compiled
+// radius R, at least 4 lanes per robot).  The group's lanes are robot-major:
+// lane li = robot (li >> lgRL), row lane q = li & (RL - 1), RL = NG / P2(N)
+// (P2: N rounded up to a power of two).  Every lane of a robot loads that
+// robot's cell and action and replays the robot-order moves (the same values
+// on all of them); row lane q senses window rows q, q + RL (n = 2R + 1 <= 7
+// rows, so at most two), loading for each the three extended-window rows a
+// move can bring into it.  The reference folds a robot's reward cells in
+// raster order (float64, :177-201): each row lane publishes its rows' cell
+// masks, and every lane of the robot runs the robot's whole fold from them.
+// Same results as sg_step_kernel<R, GPW> (which takes one lane per robot).
+// --------------------------------------------------------------------------
+template <int R, int GPW>
+__global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __restrict__ actions,
+                                                    const int32_t* __restrict__ quot,
+                                                    double* __restrict__ reward,
+                                                    uint8_t* __restrict__ done) {
+  static_assert(R >= 1 && 2 * R + 1 <= 8, "compiled radius: a row's masks fit 8 bits");
+  constexpr int NG = 64 / GPW;  // lanes per env
+  constexpr int n = 2 * R + 1;  // window rows / columns
+  constexpr int RPL = 2;        // window rows per lane (RL >= 4, n <= 7)
+  __shared__ double s_v[kEnvsPerBlock * GPW][NG];
+  __shared__ int s_x[kEnvsPerBlock * GPW][NG], s_y[kEnvsPerBlock * GPW][NG];
+  const int lane = threadIdx.x & 63;
+  const int grp = GPW == 1 ? 0 : lane / NG, li = GPW == 1 ? lane : lane & (NG - 1), gb = grp * NG;
+  const int slot_env = (threadIdx.x >> 6) * GPW + grp;
+  const int e_raw = blockIdx.x * (kEnvsPerBlock * GPW) + slot_env;
+  const bool valid = e_raw < s.B;
+  const int e = valid ? e_raw : s.B - 1;
+  const int N = s.N, W = s.W, L = s.L, RW = s.RW;
+  const int lgP2 = N <= 1 ? 0 : 32 - __clz(N - 1);
+  const int lgRL = __builtin_ctz((unsigned)NG) - lgP2;  // launch_sg_step: RL >= 4
+  const int RL = 1 << lgRL;
+  const int i = li >> lgRL, q = li & (RL - 1);
+  const bool me = valid && i < N;
+  auto gballot = [&](bool p) -> uint64_t {
+    const uint64_t m = __ballot(p);
+    return GPW == 1 ? m : (m >> gb) & low_mask(NG);
+  };
+  auto gshfl = [&](int v, int z) -> int { return __shfl(v, gb + z); };
+  auto rlane = [&](int robot) -> int { return robot << lgRL; };  // first lane of a robot
+  // ---- round 1: every load that depends only on e (clamped indices) ----
+  const size_t ri = (size_t)e * N + (i < N ? i : 0);
+  const int2 p_raw = reinterpret_cast<const int2*>(s.pos)[ri];
+  const int act_raw = actions[ri];
+  const int act0 = actions[(size_t)e * N];
+  const int g = s.env_grid[e];
+  const int q_raw = (quot ? quot : s.a_prev)[e];
+  const int ap = s.a_prev[e];
+  const int cs0 = s.currstep[e];
+  const uint32_t cc0 = s.cov_cnt[e];
+  const double dt = s.done_thresh[e];
+  asm volatile("" ::"v"(p_raw.x), "v"(p_raw.y), "v"(act_raw), "v"(act0), "v"(g), "v"(q_raw), "v"(ap),
+               "v"(cs0), "v"(cc0), "v"(dt));
+  const int my_act = me ? act_raw : 255;  // action byte i
+  const int qt = quot ? q_raw : 0;
+  const int npos = s.numpos[g];  // used at the end only
+  int dn = 0;
+  if (act0 == 255) {  // action == -1 / None (:88-90); uniform over the group
+    dn = 1;
+    if (valid && li == 0) {
+      reward[e] = 0.0;
+      done[e] = 1;
+      s.ep_pc[e] = (double)cc0 / (double)npos;
+      s.ep_len[e] = cs0;
+    }
+  } else {
+    const size_t mw = (size_t)W * RW;
+    const uint64_t* gneg = s.gneg + (size_t)g * mw;
+    const uint64_t* gpos = s.gpos + (size_t)g * mw;
+    uint64_t* cov = s.cov + (size_t)e * mw;
+    uint64_t* obst = s.obst + (size_t)e * mw;
+    int x = me ? p_raw.x : -(1 << 20), y = me ? p_raw.y : -(1 << 20);
+    const int x_old = x, y_old = y;
+    int slot = i;  // reward slot of robot i (r2c): its rank by x + y*W with scanning
+    if (s.scan) {
+      const int sc = x + y * W;
+      int rank = 0;
+      for (int j = 0; j < N; ++j) rank += gshfl(sc, rlane(j)) < sc;
+      slot = rank;
+    }
+    const int slot_act = gshfl(my_act, rlane(slot < N ? slot : 0));
+    const int u = me ? slot_act : 255;
+    int tx = x, ty = y;
+    if (u == 0) tx = x - 1;
+    else if (u == 1) tx = x + 1;
+    else if (u == 2) ty = y + 1;
+    else if (u == 3) ty = y - 1;
+    const bool inb = me && tx >= 0 && tx < W && ty >= 0 && ty < L;
+    // ---- round 2: the target's grid word and dist value, and for each of
+    // the lane's window rows the three extended rows (pre-move row x - R + jj
+    // and its neighbours) of the three planes, all from clamped addresses ----
+    const float* dpl = s.dist ? s.dist_plane : reinterpret_cast<const float*>(s.gneg);
+    const float dvr = dpl[s.dist && inb ? ((size_t)e * W + tx) * L + ty : 0];
+    const uint64_t tword = gneg[inb ? (size_t)tx * RW + (ty >> 6) : 0];
+    const int c0e = y - R - 1;
+    const int w0 = c0e >> 6, sh = c0e & 63;  // arithmetic shift: floor
+    const bool wa = w0 >= 0 && w0 < RW, wb = w0 + 1 >= 0 && w0 + 1 < RW;
+    const size_t ia = wa ? (size_t)w0 : 0, ib = wb ? (size_t)(w0 + 1) : 0;
+    auto lo32 = [](const uint64_t* p) -> uint32_t { return *reinterpret_cast<const uint32_t*>(p); };
+    uint64_t na[RPL][3], pa[RPL][3], ca[RPL][3];
+    uint32_t nb[RPL][3], pb[RPL][3], cb[RPL][3];
+    bool okr[RPL][3];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int jj = q + k * RL;                // window row
+        const int j = x - R - 1 + jj + t;         // extended row jj + t (pre-move frame)
+        okr[k][t] = me && jj < n && j >= 0 && j < W;
+        const size_t ro = (size_t)(okr[k][t] ? j : 0) * RW;
+        na[k][t] = gneg[ro + ia];
+        nb[k][t] = lo32(gneg + ro + ib);
+        pa[k][t] = gpos[ro + ia];
+        pb[k][t] = lo32(gpos + ro + ib);
+        ca[k][t] = cov[ro + ia];
+        cb[k][t] = lo32(cov + ro + ib);
+      }
+    }
+    asm volatile("" ::"v"(na[RPL - 1][2]), "v"(nb[RPL - 1][2]), "v"(pa[RPL - 1][2]), "v"(pb[RPL - 1][2]),
+                 "v"(ca[RPL - 1][2]), "v"(cb[RPL - 1][2]), "v"(dvr), "v"(tword));  // the round's one wait
+    const bool gfree = inb && !((tword >> (ty & 63)) & 1ull);
+    const double dv = (s.dist && inb && u < 4) ? (double)dvr : 0.0;
+    // ---- moves in slot order (:121-174), replayed by every lane of a robot ----
+    double v = 0.0;
+    for (int k = 0; k < N; ++k) {  // robot z = the one with slot k
+      const int z = s.scan ? ((__ffsll((unsigned long long)gballot(me && q == 0 && slot == k)) - 1) >> lgRL) : k;
+      const int zl = rlane(z);
+      const int zu = gshfl(u, zl);
+      const int zx = gshfl(tx, zl), zy = gshfl(ty, zl);
+      const int zok = gshfl((int)gfree, zl);
+      const bool occ = gballot(me && x == zx && y == zy) != 0ull;
+      if (zu < 4 && i == z) {  // not a move: nothing happens (no penalty)
+        if (zok && !occ) {
+          x = zx;
+          y = zy;
+          if (s.dist) v = v + dv;
+        } else {
+          v = v - s.pen;
+        }
+      }
+    }
+    if (me && q == 0) {
+      s_x[slot_env][i] = x;
+      s_y[slot_env][i] = y;
+    }
+    wave_sync();
+    // ---- sense (:177-201): the lane's rows; a cell with grid >= 0 is new
+    // unless covered before this step or inside a lower robot's window ----
+    const int c0 = y - R;
+    const uint32_t vm = mask32(max(0, -c0), min(n, L - c0));
+    const int mdx = x - x_old, msh = 1 + (y - y_old);  // post-move window in the extended one
+    auto fld = [&](uint64_t a, uint32_t b, bool ok) -> uint32_t {
+      const uint64_t A = (ok && wa) ? a : 0ull, Bw = (ok && wb) ? (uint64_t)b : 0ull;
+      return (uint32_t)(sh ? (A >> sh) | (Bw << (64 - sh)) : A);
+    };
+    uint32_t rneg[RPL], rpos[RPL], rcov[RPL], rnw[RPL], rge[RPL];
+    bool rin[RPL];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const int jj = q + k * RL;
+      const int j = x - R + jj;
+      const int t = 1 + mdx;  // post-move row jj is extended row jj + 1 + mdx
+      const uint64_t an = t == 0 ? na[k][0] : (t == 1 ? na[k][1] : na[k][2]);
+      const uint32_t bn = t == 0 ? nb[k][0] : (t == 1 ? nb[k][1] : nb[k][2]);
+      const uint64_t ap_ = t == 0 ? pa[k][0] : (t == 1 ? pa[k][1] : pa[k][2]);
+      const uint32_t bp = t == 0 ? pb[k][0] : (t == 1 ? pb[k][1] : pb[k][2]);
+      const uint64_t ac = t == 0 ? ca[k][0] : (t == 1 ? ca[k][1] : ca[k][2]);
+      const uint32_t bc = t == 0 ? cb[k][0] : (t == 1 ? cb[k][1] : cb[k][2]);
+      const bool ok = t == 0 ? okr[k][0] : (t == 1 ? okr[k][1] : okr[k][2]);
+      rin[k] = me && jj < n && j >= 0 && j < W;
+      rneg[k] = (fld(an, bn, ok) >> msh) & vm;
+      rpos[k] = (fld(ap_, bp, ok) >> msh) & vm;
+      rcov[k] = (fld(ac, bc, ok) >> msh) & vm;
+      uint32_t lower = 0;
+      for (int m = 0; m < N; ++m) {  // robots m < i
+        const int xm = s_x[slot_env][m], ym = s_y[slot_env][m];
+        const uint32_t cm = mask32(max(0, ym - R - c0), min(n, ym + R + 1 - c0));
+        lower |= (m < i && abs(j - xm) <= R) ? cm : 0u;
+      }
+      rge[k] = rin[k] ? (vm & ~rneg[k]) : 0u;
+      rnw[k] = rge[k] & ~rcov[k] & ~lower;
+      cnt += __popc(rnw[k]);
+    }
+    // the lane's rows' masks (nw, ge0, fpos: one byte each), row k at bits
+    // 24k..; the robot's row jj is in lane jj & (RL - 1), slot jj >> lgRL
+    uint64_t pub64 = 0;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k)
+      pub64 |= (uint64_t)(rnw[k] | (rge[k] << 8) | ((rpos[k] & 0xFFu) << 16)) << (24 * k);
+    const double mfp = -s.fpen;
+#pragma unroll
+    for (int jj = 0; jj < n; ++jj) {
+      const int src = gb + rlane(i < N ? i : 0) + (jj & (RL - 1));
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)pub64, src);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(pub64 >> 32), src);
+      const uint64_t w = (uint64_t)lo | ((uint64_t)hi << 32);
+      const uint32_t row = (uint32_t)(w >> (24 * (jj >> lgRL)));
+      const uint32_t nw = row & 0xFFu, ge0 = (row >> 8) & 0xFFu, fpos = (row >> 16) & 0xFFu;
+      // raster fold, branch-free: v - fpen == v + (-fpen) in IEEE
+#pragma unroll
+      for (int b = 0; b < n; ++b) {
+        const double tv = ((nw >> b) & 1u) ? (((fpos >> b) & 1u) ? 1.0 : 0.0) : mfp;
+        const double vt = v + tv;
+        v = ((ge0 >> b) & 1u) ? vt : v;
+      }
+    }
+    // ---- phase B: maps and state planes of the lane's rows ----
+    const size_t WL = (size_t)W * L;
+    uint8_t* pl = s.planes + (size_t)e * (s.P + 2) * WL;
+    uint8_t* pl_obst = pl + (size_t)s.P * WL;
+    uint8_t* pl_free = pl + (size_t)(s.P + 1) * WL;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      if (!rin[k]) continue;
+      const int j = x - R + q + k * RL;
+      // OR only the bits not covered before this step (covered bits are
+      // cleared only by a reset), so re-sensed rows cost no atomic
+      const uint32_t ncov = rge[k] & ~rcov[k];
+      or_field(cov + (size_t)j * RW, RW, c0, ncov);
+      or_field(obst + (size_t)j * RW, RW, c0, rneg[k]);
+      uint8_t* row_o = pl_obst + (size_t)j * L + c0;
+      uint8_t* row_f = pl_free + (size_t)j * L + c0;
+      // a cell covered before this step already holds 0 in _free: only new
+      // cells and obstacles are stored
+      const uint32_t st = ncov | rneg[k];
+#pragma unroll
+      for (int b = 0; b < n; ++b) {  // obstacle -> 1 in layer P, else 0 in _free
+        const bool ob = (rneg[k] >> b) & 1u;
+        uint8_t* dst = (ob ? row_o : row_f) + b;
+        if ((st >> b) & 1u) *dst = ob ? 1 : 0;
+      }
+    }
+    const bool lead = me && q == 0;
+    // robot cells: clear the old one, set the new one (use_scanning: a cell
+    // vacated by one robot and entered by another keeps its 1)
+    const bool moved = lead && (x != x_old || y != y_old);
+    const size_t lay = (size_t)(s.scan ? 0 : i) * WL;
+    bool reoccupied = false;
+    if (s.scan && lead)
+      for (int m = 0; m < N; ++m) reoccupied |= s_x[slot_env][m] == x_old && s_y[slot_env][m] == y_old;
+    if (moved && !reoccupied) pl[lay + (size_t)x_old * L + y_old] = 0;
+    if (moved) pl[lay + (size_t)x * L + y] = 1;
+    // motion_penalty(a) on every slot (:203-208, 227-243)
+    if ((qt < 0 || qt >= 4) && valid && li == 0) atomicOr(s.err, ERR_KEY);
+    v = v + ((qt == ap) ? 0.0 : -1.0);
+    if (lead) {
+      s_v[slot_env][slot] = v;
+      s.pos[((size_t)e * N + i) * 2] = x;
+      s.pos[((size_t)e * N + i) * 2 + 1] = y;
+    }
+#pragma unroll
+    for (int o = NG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);  // group sum
+    wave_sync();
+    if (valid && li == 0) {
+      double total = np_pairwise_sum(s_v[slot_env], N);
+      const int cs = cs0 + 1;
+      const uint32_t cc = cc0 + (uint32_t)cnt;
+      const double pc = (double)cc / (double)npos;
+      const bool cond = (dt < 1.0 ? dt : 1.0) <= pc;  // min(_done_thresh, 1) <= percent_covered()
+      if (cond) total = total + s.term;
+      if (cond) s.done_thresh[e] = dt + s.dincr;  // done() (:408-411)
+      dn = cond || (s.maxsteps > 0 && cs == s.maxsteps);
+      s.a_prev[e] = qt;
+      s.currstep[e] = cs;
+      s.cov_cnt[e] = cc;
+      reward[e] = total;
+      done[e] = (uint8_t)dn;
+      if (dn) {  // the episode record (Utils/utils.py:138-141)
+        s.ep_pc[e] = pc;
+        s.ep_len[e] = cs;
+      }
+    }
+  }
+  uint64_t rs = __ballot(s.auto_reset && valid && li == 0 && dn != 0);
+  if (rs) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the step's map ORs land first
+    const int e0 = blockIdx.x * (kEnvsPerBlock * GPW) + (int)(threadIdx.x >> 6) * GPW;
+    for (; rs; rs &= rs - 1) {
+      const int gj = (__ffsll((unsigned long long)rs) - 1) / NG;
+      sg_reset_env(s, e0 + gj, lane, nullptr);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
 // get_state (:305-317) planes: full rewrite of the uint8 layers (after a
 // reset / state upload) and the distance layer of every env.
 // --------------------------------------------------------------------------
@@ -1166,6 +1453,31 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   }();
   const int R = force_generic ? -1 : (E->s.r >= 1 && E->s.r <= 3 ? E->s.r : -1);
   decltype(&mcs::sg_step_kernel<-1, 1>) kern = nullptr;
+  // compiled radius and at least 4 lanes per robot: the row-parallel kernel
+  // (MARLCOV_SG_ROWS=0 keeps one lane per robot: A/B and parity in both)
+  static const bool rows_on = [] {
+    const char* v = getenv("MARLCOV_SG_ROWS");
+    return !(v && atoi(v) == 0);
+  }();
+  int p2 = 1;
+  while (p2 < E->s.N) p2 *= 2;
+  if (rows_on && R >= 1 && 4 * p2 <= 64) {
+    gpw = 1;
+    while (2 * gpw <= gpw_cap && 4 * p2 * 2 * gpw <= 64) gpw *= 2;
+#define SG_PICK_ROWS(RR)                                             \
+  switch (gpw) {                                                     \
+    case 1: kern = mcs::sg_step_rows<RR, 1>; break;                  \
+    case 2: kern = mcs::sg_step_rows<RR, 2>; break;                  \
+    case 4: kern = mcs::sg_step_rows<RR, 4>; break;                  \
+    default: kern = mcs::sg_step_rows<RR, 8>; break;                 \
+  }
+    switch (R) {
+      case 1: SG_PICK_ROWS(1); break;
+      case 2: SG_PICK_ROWS(2); break;
+      default: SG_PICK_ROWS(3); break;
+    }
+#undef SG_PICK_ROWS
+  }
 #define SG_PICK(RR)                                                  \
   switch (gpw) {                                                     \
     case 1: kern = mcs::sg_step_kernel<RR, 1>; break;                \
@@ -1174,11 +1486,13 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
     case 8: kern = mcs::sg_step_kernel<RR, 8>; break;                \
     default: kern = mcs::sg_step_kernel<RR, 16>; break;              \
   }
-  switch (R) {  // compile-time radii of the reference configs (staged window)
-    case 1: SG_PICK(1); break;
-    case 2: SG_PICK(2); break;
-    case 3: SG_PICK(3); break;
-    default: SG_PICK(-1); break;
+  if (kern == nullptr) {
+    switch (R) {  // compile-time radii of the reference configs (staged window)
+      case 1: SG_PICK(1); break;
+      case 2: SG_PICK(2); break;
+      case 3: SG_PICK(3); break;
+      default: SG_PICK(-1); break;
+    }
   }
 #undef SG_PICK
   const int per_block = mcs::kEnvsPerBlock * gpw;
