@@ -691,6 +691,18 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
     uint32_t rneg[RPL], rpos[RPL], rcov[RPL], rnw[RPL], rge[RPL];
     bool rin[RPL];
     int cnt = 0;
+    // lower robots' window columns (relative to c0) and rows, once per robot
+    // (at most NG / 4 robots: RL >= 4)
+    constexpr int NMAX = NG / 4;
+    uint32_t lcm[NMAX];
+    int lxm[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; ++m) {
+      const bool lo = m < N && m < i;
+      const int xm = s_x[slot_env][m < N ? m : 0], ym = s_y[slot_env][m < N ? m : 0];
+      lcm[m] = lo ? mask32(max(0, ym - R - c0), min(n, ym + R + 1 - c0)) : 0u;
+      lxm[m] = xm;
+    }
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const int jj = q + k * RL;
@@ -708,11 +720,8 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
       rpos[k] = (fld(ap_, bp, ok) >> msh) & vm;
       rcov[k] = (fld(ac, bc, ok) >> msh) & vm;
       uint32_t lower = 0;
-      for (int m = 0; m < N; ++m) {  // robots m < i
-        const int xm = s_x[slot_env][m], ym = s_y[slot_env][m];
-        const uint32_t cm = mask32(max(0, ym - R - c0), min(n, ym + R + 1 - c0));
-        lower |= (m < i && abs(j - xm) <= R) ? cm : 0u;
-      }
+#pragma unroll
+      for (int m = 0; m < NMAX; ++m) lower |= (abs(j - lxm[m]) <= R) ? lcm[m] : 0u;  // robots m < i
       rge[k] = rin[k] ? (vm & ~rneg[k]) : 0u;
       rnw[k] = rge[k] & ~rcov[k] & ~lower;
       cnt += __popc(rnw[k]);
@@ -757,13 +766,12 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
       uint8_t* row_o = pl_obst + (size_t)j * L + c0;
       uint8_t* row_f = pl_free + (size_t)j * L + c0;
       // a cell covered before this step already holds 0 in _free: only new
-      // cells and obstacles are stored
-      const uint32_t st = ncov | rneg[k];
+      // cells (0 in _free) and obstacles (1 in layer P) are stored; fixed row
+      // bases, so each store's column rides in its offset field
 #pragma unroll
-      for (int b = 0; b < n; ++b) {  // obstacle -> 1 in layer P, else 0 in _free
-        const bool ob = (rneg[k] >> b) & 1u;
-        uint8_t* dst = (ob ? row_o : row_f) + b;
-        if ((st >> b) & 1u) *dst = ob ? 1 : 0;
+      for (int b = 0; b < n; ++b) {
+        if ((rneg[k] >> b) & 1u) row_o[b] = 1;
+        if ((ncov >> b) & 1u) row_f[b] = 0;
       }
     }
     const bool lead = me && q == 0;
