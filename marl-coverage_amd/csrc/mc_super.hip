@@ -1163,6 +1163,7 @@ struct SgEnv {
   int dist_nt = 256;
   bool grids_set = false;
   bool stale = true;  // the dist layer does not describe the current maps
+  bool rows = true;   // row-parallel step kernel when it applies (MARLCOV_SG_ROWS)
   std::vector<void*> allocs;
 };
 
@@ -1280,6 +1281,10 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
   {
     const char* fd = getenv("MARLCOV_SG_FULL_DIST");
     s.dist_full = fd && atoi(fd) == 1;
+    // MARLCOV_SG_ROWS=0: one lane per robot instead of the row-parallel step
+    // kernel (read per handle: the parity suite runs both)
+    const char* rw = getenv("MARLCOV_SG_ROWS");
+    E->rows = !(rw && atoi(rw) == 0);
   }
   s.seed = c.seed;
   s.env0 = c.env_offset;
@@ -1462,14 +1467,10 @@ int mc_sg_step(void* env, const uint8_t* dev_actions, const int32_t* dev_quot, d
   const int R = force_generic ? -1 : (E->s.r >= 1 && E->s.r <= 3 ? E->s.r : -1);
   decltype(&mcs::sg_step_kernel<-1, 1>) kern = nullptr;
   // compiled radius and at least 4 lanes per robot: the row-parallel kernel
-  // (MARLCOV_SG_ROWS=0 keeps one lane per robot: A/B and parity in both)
-  static const bool rows_on = [] {
-    const char* v = getenv("MARLCOV_SG_ROWS");
-    return !(v && atoi(v) == 0);
-  }();
+  // (MARLCOV_SG_ROWS=0 at create keeps one lane per robot)
   int p2 = 1;
   while (p2 < E->s.N) p2 *= 2;
-  if (rows_on && R >= 1 && 4 * p2 <= 64) {
+  if (E->rows && R >= 1 && 4 * p2 <= 64) {
     gpw = 1;
     while (2 * gpw <= gpw_cap && 4 * p2 * 2 * gpw <= 64) gpw *= 2;
 #define SG_PICK_ROWS(RR)                                             \

@@ -120,6 +120,20 @@ BATCH_CASES = {
 }
 
 
+# the same cases with the one-lane-per-robot step kernel and with the whole
+# distance layer rewritten every step (both read when the handle is created)
+ALT_MODES = {"lane_per_robot": {"MARLCOV_SG_ROWS": "0"}, "full_dist_layer": {"MARLCOV_SG_FULL_DIST": "1"}}
+ALT_CASES = ["n4_r2_dist", "scan_n6_r1_dist", "zero_cells_n3_r3", "n16_r2_dist", "done_incr_small"]
+
+
+@pytest.mark.parametrize("mode", sorted(ALT_MODES))
+@pytest.mark.parametrize("name", ALT_CASES)
+def test_super_batch_alt_modes(torch_cuda, monkeypatch, name, mode):
+    for k, v in ALT_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    test_super_batch_matches_oracle(torch_cuda, name)
+
+
 @pytest.mark.parametrize("name", sorted(BATCH_CASES))
 def test_super_batch_matches_oracle(torch_cuda, name):
     import marlcov
