@@ -109,6 +109,13 @@ BATCH_CASES = {
                     lambda rs: bern(rs, 12, 12, 0.1), 4, 20),
     "n33_wide_window": (base_cfg(numrobot=33, sensor_config={"num_lasers": 7, "range": 3}),
                         lambda rs: bern(rs, 30, 30, 0.1), 2, 10),
+    # the accepted maxima (DESIGN.md §7 limits): 64 robots; lidar range 27
+    # (8 x 8 window tiles, 64-bit march rows) with egoradius 15
+    "limit_n64_agents": (base_cfg(numrobot=64, collision_penalty=1.5,
+                                  sensor_config={"num_lasers": 7, "range": 3}),
+                         lambda rs: bern(rs, 40, 40, 0.1), 2, 12),
+    "limit_range27_ego15": (base_cfg(numrobot=4, egoradius=15, sensor_config={"num_lasers": 13, "range": 27}),
+                            lambda rs: bern(rs, 90, 70, 0.1), 2, 10),
     # dijkstra_input obs layer: BFS path to the nearest
     # unexplored cell; long episodes on small grids reach long paths
     "dijkstra_square_r1": (base_cfg(numrobot=2, dijkstra_input=1, sensor_type="square_sensor",
