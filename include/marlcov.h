@@ -184,8 +184,10 @@ int mc_random_actions(void* env, uint64_t seed, int32_t step, uint8_t* dev_actio
 
 /* Name of the env-kernel instantiation the next mc_step / mc_reset launches
  * (compiled shape or the generic kernel, lanes per workgroup, envs per
- * workgroup), e.g. "env_kernel<64,2,u32,C2>".  Diagnostic: lets tests show
- * which specialisation they cover.  The string is static. */
+ * workgroup), e.g. "env_kernel<64,2,u32,C2>", followed by " +fan(S/P)" when
+ * a dense lidar set marches by sectors (S sectors, P special beams) instead
+ * of by rays.  Diagnostic: lets tests show which specialisation they cover.
+ * The string stays valid until the calling thread's next call. */
 const char* mc_kernel_variant(void* env);
 
 /* Which pool grid each env uses (int32 [B], device). */

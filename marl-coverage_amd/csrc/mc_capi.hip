@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "marlcov.h"
@@ -80,6 +81,8 @@ struct Env {
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
   void* bits_buf = nullptr;   // u64 [beam_count][max(Wp, Lp)]
+  void* fan_buf = nullptr;    // u32 [State::fan_words]: fan march data (dense beam sets)
+  size_t fan_cap = 0;         // words allocated in fan_buf
   int beam_count = 0;
   bool grids_set = false;
   std::vector<void*> allocs;
@@ -420,6 +423,7 @@ void mc_destroy(void* env) {
   for (void* p : E->allocs) (void)hipFree(p);
   if (E->beams_buf) (void)hipFree(E->beams_buf);
   if (E->bits_buf) (void)hipFree(E->bits_buf);
+  if (E->fan_buf) (void)hipFree(E->fan_buf);
   delete E;
 }
 
@@ -427,6 +431,101 @@ int mc_query(void* env, mc_layout* out) {
   if (!env || !out) return fail(MC_EINVAL, "mc_query: null argument");
   *out = as_env(env)->lay;
   return MC_OK;
+}
+
+// Fan march data of a dense beam set (mc_env_kernel.hip fan_march, layout in
+// mc_internal.h State::fan_data).  The beams with one step pattern for every
+// start are grouped by octant class (major axis, major sign, minor sign;
+// minor sign 0 counts as +), ordered by their minor offsets, and cut greedily
+// into sectors of up to kFanS beams whose offsets differ by 0 or 1 between
+// neighbours at every step; the classes are interleaved, so the sectors of
+// one march instruction mark different lines.  Beams with start-dependent
+// patterns (Beam::axis bit 1) become one-beam special sectors.  Returns false
+// (ray march) for sparse sets: fewer than 64 beams (dense_beams), or fewer
+// than two beams per sector on average.
+static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lanes,
+                      std::vector<uint32_t>& out, int& nsec, int& nspec) {
+  const int nb = (int)bt.size();
+  if (nb < 64 || kmax > 27) return false;
+  auto off = [](const mc::Beam& o, int k) {  // signed minor offset of step k
+    return o.msign * __builtin_popcount(o.bits & ((1u << k) - 1u));
+  };
+  std::vector<std::vector<int>> cls(8);
+  std::vector<int> spec;
+  for (int b = 0; b < nb; ++b) {
+    const mc::Beam& o = bt[b];
+    if (o.axis & 2) { spec.push_back(b); continue; }
+    cls[(o.axis & 1) * 4 + (o.sign < 0 ? 2 : 0) + (o.msign < 0 ? 1 : 0)].push_back(b);
+  }
+  std::vector<std::vector<std::vector<int>>> secs(8);
+  size_t most = 0;
+  for (int c = 0; c < 8; ++c) {
+    std::vector<int>& v = cls[c];
+    std::sort(v.begin(), v.end(), [&](int p, int q) {
+      for (int k = kmax; k >= 1; --k) {
+        const int a = off(bt[p], k), d = off(bt[q], k);
+        if (a != d) return a < d;
+      }
+      return p < q;
+    });
+    for (int b : v) {
+      std::vector<std::vector<int>>& S = secs[c];
+      bool join = !S.empty() && (int)S.back().size() < mc::kFanS;
+      for (int k = 1; join && k <= kmax; ++k) {
+        const int d = off(bt[b], k) - off(bt[S.back().back()], k);
+        join = d == 0 || d == 1;
+      }
+      if (join) S.back().push_back(b);
+      else S.push_back({b});
+    }
+    most = std::max(most, secs[c].size());
+  }
+  std::vector<const std::vector<int>*> order;
+  for (size_t i = 0; i < most; ++i)
+    for (int c = 0; c < 8; ++c)
+      if (i < secs[c].size()) order.push_back(&secs[c][i]);
+  nsec = (int)order.size();
+  nspec = (int)spec.size();
+  if (2 * (nsec + nspec) > nb || N * nspec > lanes) return false;
+  out.assign(mc::kFanLutBytes / 4, 0u);
+  uint8_t* lut = reinterpret_cast<uint8_t*>(out.data());
+  for (int D = 0; D < 32; ++D) {
+    int r[mc::kFanS] = {0};  // cell of beam i
+    for (int i = 1; i < mc::kFanS; ++i) r[i] = r[i - 1] + ((D >> (i - 1)) & 1);
+    for (int A = 0; A < 64; ++A) {
+      int lit = 0, kill = 0;
+      for (int i = 0; i < mc::kFanS; ++i) {
+        if ((A >> i) & 1) lit |= 1 << r[i];      // spread: beams A -> their cells
+        if ((A >> r[i]) & 1) kill |= 1 << i;     // expand: cells A -> the beams on them
+      }
+      lut[D * 64 + A] = (uint8_t)lit;
+      lut[2048 + D * 64 + A] = (uint8_t)kill;
+    }
+  }
+  auto cbits = [](const mc::Beam& o) {
+    return ((o.axis & 1) ? (uint32_t)mc::FAN_COLS : 0u) | (o.sign < 0 ? (uint32_t)mc::FAN_NEG : 0u);
+  };
+  for (const std::vector<int>* S : order) {
+    const std::vector<int>& v = *S;
+    out.push_back(cbits(bt[v[0]]));
+    for (int k = 1; k <= kmax; ++k) {
+      const int lo = off(bt[v[0]], k);
+      uint32_t D = 0, valid = 0;
+      for (size_t j = 0; j < v.size(); ++j) {
+        if (j + 1 < v.size() && off(bt[v[j + 1]], k) != off(bt[v[j]], k)) D |= 1u << j;
+        if (bt[v[j]].K >= k) valid |= 1u << j;
+      }
+      out.push_back((uint32_t)(lo + 32) | (D << 6) | (valid << 16));
+    }
+  }
+  for (int b : spec) {
+    out.push_back((uint32_t)b);
+    out.push_back(cbits(bt[b]));
+    out.push_back((uint32_t)bt[b].msign);
+    out.push_back((uint32_t)bt[b].K);
+  }
+  while (out.size() % 4) out.push_back(0u);
+  return true;
 }
 
 int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
@@ -557,6 +656,35 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     k1 |= 1u << (3 * (dx + 1) + (dy + 1));
   }
   E->s.beam_k1 = E->s.beam_common && !getenv("MARLCOV_NO_K1") ? k1 : 0u;
+  // fan march of a dense set (after nt / epw: they bound the special lanes);
+  // MARLCOV_FAN=0 or MARLCOV_BEAM_TABLE keep the ray march (parity A/B)
+  {
+    std::vector<uint32_t> fd;
+    int nsec = 0, nspec = 0;
+    const char* fv = getenv("MARLCOV_FAN");
+    bool on = !getenv("MARLCOV_BEAM_TABLE") && !(fv && fv[0] == '0') &&
+              build_fan(bt, kmax, E->s.N, E->nt / E->epw, fd, nsec, nspec);
+    const int rb = E->s.TW <= 4 ? 4 : 8;
+    if (on && mc::env_lds_bytes(E->s.N, E->s.TW, num_beams, rb,
+                                mc::fan_lds_bytes(E->s.N, E->s.TW, rb, nspec, kmax, (int)fd.size())) > 65536)
+      on = false;
+    if (on) {
+      if (fd.size() > E->fan_cap) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (E->fan_buf) (void)hipFree(E->fan_buf);
+        E->fan_buf = nullptr;
+        E->fan_cap = 0;
+        HIP_TRY(hipMalloc(&E->fan_buf, fd.size() * 4));
+        E->fan_cap = fd.size();
+      }
+      HIP_TRY(hipMemcpy(E->fan_buf, fd.data(), fd.size() * 4, hipMemcpyHostToDevice));
+      E->s.fan_data = (const uint32_t*)E->fan_buf;
+    }
+    E->s.fan_nsec = on ? nsec : 0;
+    E->s.fan_nspec = on ? nspec : 0;
+    E->s.fan_kt = on ? kmax : 0;
+    E->s.fan_words = on ? (int)fd.size() : 0;
+  }
   E->beams_set = true;
   return MC_OK;
 }
@@ -612,7 +740,13 @@ const char* mc_kernel_variant(void* env) {
     fail(MC_EINVAL, "mc_kernel_variant: null env");
     return "";
   }
-  return mc::env_variant(E->s, E->nt, launch_epw(E));
+  // the lidar's march: "+fan(S/P)" = fan_march over S sectors and P special
+  // beams (dense beam sets), else the ray march
+  thread_local std::string name;
+  name = mc::env_variant(E->s, E->nt, launch_epw(E));
+  if (E->s.sensor == MC_SENSOR_LIDAR && E->s.fan_nsec + E->s.fan_nspec > 0)
+    name += " +fan(" + std::to_string(E->s.fan_nsec) + "/" + std::to_string(E->s.fan_nspec) + ")";
+  return name.c_str();
 }
 
 int mc_set_env_grids(void* env, const int32_t* dev_env_grid, void* stream) {

@@ -61,6 +61,9 @@ struct Scal {
 };
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
 
+// the lidar marches by sectors (fan_march) rather than by rays
+__device__ __forceinline__ bool fan_on(const State& s) { return s.sensor == 0 && s.fan_nsec + s.fan_nspec > 0; }
+
 // One env slot's LDS.  Tile planes are [N][TW][TW] u64 in the agent's block
 // coordinates.  Row planes are [N][8*TW+1] WT: row lx of agent a's block, bit ly
 // = cell (8*bx + lx, 8*by + ly); the lidar march and the moves read them.
@@ -73,6 +76,13 @@ template <typename WT>
 struct Lds {
   uint64_t *neg, *pos, *fold, *oold, *fp, *op;
   WT *negr, *fldr, *fpr;
+  // fan march (dense beams): column planes (word ly of agent a at
+  // row_word(a, ly), bit lx = cell (8*bx + lx, 8*by + ly)) of neg, marks and
+  // seen cells, the same distances apart as negr / fpr / fldr; fan data
+  // (LUTs, sector records, special-beam records) and the per-(agent,
+  // special beam) entries.  Null without the fan.
+  WT *cneg, *cmark, *cseen;
+  uint32_t *fan, *fspec;
   Beam* beams;
   int32_t *x0, *y0, *x, *y;  // pre-move / post-move cells
   int32_t *bx, *by;          // tile-block origin (tile units) of each agent
@@ -102,8 +112,19 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   L.fpr = L.negr + rows;
   L.fldr = L.fpr + rows;
   q += (((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15;
+  L.cneg = L.cmark = L.cseen = nullptr;
+  L.fan = L.fspec = nullptr;
   L.beams = reinterpret_cast<Beam*>(q);
-  q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
+  if (fan_on(s)) {
+    L.cneg = reinterpret_cast<WT*>(q);
+    L.cmark = L.cneg + rows;
+    L.cseen = L.cmark + rows;
+    L.fan = reinterpret_cast<uint32_t*>(q + ((((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15));
+    L.fspec = L.fan + s.fan_words;
+    q += (fan_lds_bytes(s.N, s.TW, (int)sizeof(WT), s.fan_nspec, s.fan_kt, s.fan_words) + 15) & ~(size_t)15;
+  } else {
+    q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
+  }
   L.x0 = reinterpret_cast<int32_t*>(q);
   L.y0 = L.x0 + s.N;
   L.x = L.y0 + s.N;
@@ -379,8 +400,18 @@ __device__ __forceinline__ void stage_load(const State& s, const Ctx<NT, EPW, WT
   I.masks = load_masks;
 }
 
+// 8x8 bit-matrix transpose of a tile (bit 8r + c <-> bit 8c + r)
+__device__ __forceinline__ uint64_t transpose8(uint64_t x) {
+  uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x ^= t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x ^= t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  return x ^ t ^ (t << 28);
+}
+
 // round trip 2, landing: the grid tiles into the row planes (and the tile
-// planes for the square sensor)
+// planes for the square sensor; the column planes for the fan march)
 template <int NT, int EPW, typename WT, int KI>
 __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW, WT>& C, Items<KI>& I) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -412,10 +443,23 @@ __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW,
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
+      const uint64_t ft = (known && I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
-        const uint64_t ft = (I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
 #pragma unroll
         for (int r = 0; r < 8; ++r) fb[off + r * rs] = (uint8_t)(ft >> (8 * r));
+      }
+      if (fan_on(s)) {
+        // fan march: the column planes too -- byte ti of words 8*tj .. 8*tj+7
+        // are the transposed tile's bytes
+        uint8_t* cb = reinterpret_cast<uint8_t*>(L.cneg);
+        uint8_t* sb = reinterpret_cast<uint8_t*>(L.cseen);
+        const size_t coff = (size_t)row_word<WT>(s, I.a[k], 8 * I.tj[k]) * sizeof(WT) + I.ti[k];
+        const uint64_t nT = transpose8(nt), fT = transpose8(ft);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          cb[coff + r * rs] = (uint8_t)(nT >> (8 * r));
+          sb[coff + r * rs] = (uint8_t)(fT >> (8 * r));
+        }
       }
     }
   }
@@ -461,8 +505,10 @@ template <int NT, int EPW, typename WT>
 __device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   if (s.sensor != 0) return;
+  const bool fan = fan_on(s);
   for (int r = C.sub; r < row_plane_words(s.N, s.TW, (int)sizeof(WT)); r += LPE) {
     C.L.fpr[r] = 0;
+    if (fan) C.L.cmark[r] = 0;
   }
 }
 
@@ -724,7 +770,126 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
   return on;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int KN>
+// --------------------------------------------------------------------------
+// Fan march: dense beam sets (lidar.py:34-63).  Every beam whose step bits
+// are the same from every start (Beam::axis bit 1 clear) belongs to an octant
+// class (major axis and sign; mc_set_beam_table) and all of a class's beams
+// sit on the same line at step k: the row (or column) k cells from the robot.
+// A sector is up to kFanS beams of one class, ordered by minor offset, that
+// are never more than one cell apart at any step, so at step k its beams
+// cover the cells lo(k) .. lo(k) + 5 of the line and the beam -> cell map is
+// the monotone map D(k).  A lane marches one (agent, sector) with the live
+// beams A as bits: the cells lit at step k are spread[D][A] (each is marked:
+// free up to the first obstacle, and that obstacle), and the beams whose cell
+// is an obstacle, expand[D][F], leave A.  One step is a few bit operations
+// and three LUT / table reads for up to six beams, where the ray march spends
+// a dozen VALU operations per ray and step.  Beams with start-dependent bits
+// (C4: 270 and 315 degrees) march as one-beam sectors whose entries the lane
+// builds from the start word of its robot's post-move cell.  Column lines read
+// and mark the column planes (cneg / cmark / cseen), which the stage fills
+// with transposed tiles and gather_marks transposes back.  Cells the agent has
+// seen (cseen / fldr) are not marked again (dense_beams).
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const lds_char*)(const char*)p;
+}
+template <typename T>
+__device__ __forceinline__ T* lds_ptr(uint32_t a) {
+  return reinterpret_cast<T*>((char*)((lds_char*)(uintptr_t)a));
+}
+
+template <int NT, int EPW, typename WT, int KM>
+__device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>& C) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int SU = 5;  // steps per batch: reads, then the live-beam chain, then marks
+  const Lds<WT>& L = C.L;
+  const int N = s.N;
+  const int kt = KM > 0 ? KM : s.fan_kt;
+  const int nsec = s.fan_nsec, nspec = s.fan_nspec;
+  const int qs = N * nsec;  // first special lane-sector
+  const int total = qs + N * nspec;
+  const uint32_t MD = (uint32_t)(row_plane_words(N, s.TW, (int)sizeof(WT)) * (int)sizeof(WT));  // neg -> marks
+  const uint32_t lut = lds_addr(L.fan);  // spread at lut, expand at lut + 2048
+  const uint32_t* sec = L.fan + kFanLutBytes / 4;
+  const uint32_t* sdesc = sec + nsec * (kt + 1);
+  // the lane that marches special i (lane-sector qs + i; mc_set_beam_table
+  // keeps N * nspec <= lanes per env, one per lane) loads the start word of
+  // its robot's post-move cell now, for a later pass
+  uint32_t spw = 0;
+  if (nspec > 0) {
+    int i = C.sub - qs % LPE;
+    if (i < 0) i += LPE;
+    if (i < N * nspec) {
+      const int a = i / nspec, j = i - a * nspec;
+      const uint32_t* d = sdesc + 4 * j;
+      const int c0 = (d[1] & FAN_COLS) ? L.x[a] : L.y[a];  // the minor coordinate
+      spw = (uint32_t)s.beam_bits[(size_t)d[0] * s.bcmax + c0];
+    }
+  }
+  for (int q = C.sub; q < total; q += LPE) {
+    int a;
+    const uint32_t* T;
+    if (q < qs) {
+      const int sg = q / N;
+      a = q - sg * N;
+      T = sec + sg * (kt + 1);
+    } else {  // special beam: a one-beam sector (D = 0) with this start's steps
+      const int i = q - qs;
+      a = i / nspec;
+      const uint32_t* d = sdesc + 4 * (i - a * nspec);
+      const int msign = (int)d[2], K = (int)d[3];
+      uint32_t* W = L.fspec + i * (kt + 1);
+      W[0] = d[1];
+      int lo = 0;
+      for (int k = 1; k <= kt; ++k) {
+        lo += ((spw >> (k - 1)) & 1u) ? msign : 0;
+        W[k] = (uint32_t)(lo + 32) | (K >= k ? (1u << 16) : 0u);
+      }
+      T = W;
+    }
+    const uint32_t desc = T[0];
+    const bool cols = (desc & FAN_COLS) != 0;
+    const int lx = L.x[a] - 8 * L.bx[a], ly = L.y[a] - 8 * L.by[a];
+    // the line's word in the neg plane (row lx + sign k, or column ly + sign k);
+    // marks MD bytes on, seen cells 2 MD on
+    const uint32_t P0 = lds_addr(cols ? L.cneg : L.negr) + (uint32_t)row_word<WT>(s, a, cols ? ly : lx) * sizeof(WT);
+    const int stride = ((desc & FAN_NEG) ? -1 : 1) * row_step<WT>(s) * (int)sizeof(WT);
+    const int bb = (cols ? lx : ly) - 32;  // bit of the cell at minor offset lo: bb + (lo + 32)
+    uint32_t A = 63u;
+    for (int k0 = 1; k0 <= kt; k0 += SU) {
+      uint32_t e[SU], F[SU], SN[SU], kill[SU], lit[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        e[u] = F[u] = SN[u] = 0;
+        if (KM > 0 ? (k0 + u <= KM) : (k0 + u <= kt)) {
+          e[u] = T[k0 + u];
+          const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
+          const int sh = bb + (int)(e[u] & 63u);
+          F[u] = (uint32_t)(*lds_ptr<const WT>(P) >> sh) & 63u;
+          SN[u] = (uint32_t)(*lds_ptr<const WT>(P + 2 * MD) >> sh) & 63u;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) kill[u] = *lds_ptr<const uint8_t>(lut + 2048 + ((e[u] & 0x7C0u) | F[u]));
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        A &= e[u] >> 16;  // in range (a step past the trip count has e = 0)
+        lit[u] = *lds_ptr<const uint8_t>(lut + ((e[u] & 0x7C0u) | A));
+        A &= ~kill[u];
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const uint32_t nm = lit[u] & ~SN[u];
+        if (nm) {
+          const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
+          lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)(e[u] & 63u)));
+        }
+      }
+    }
+  }
+}
+
+template <int NT, int EPW, typename WT, int SUK, int KN, int KM = 0>
 __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   constexpr int RPL = Ctx<NT, EPW, WT>::RPL;
@@ -746,6 +911,10 @@ __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C)
       const uint32_t b3 = k1 ? (k1 >> (3 * (dx + 1))) & 7u : 2u;  // cells y-1, y, y+1
       const int lx = L.x[a] - 8 * L.bx[a] + dx, ly = L.y[a] - 8 * L.by[a] - 1;  // ly >= H >= 1
       if (b3) lds_or<WT>(&L.fpr[row_word<WT>(s, a, lx)], (WT)b3 << ly);
+    }
+    if (fan_on(s)) {
+      fan_march<NT, EPW, WT, KM>(s, C);
+      return;
     }
     WT* sink = L.sink + (threadIdx.x & 63);
     const uint32_t sink_m = (uint32_t)(uintptr_t)(const lds_char*)(const char*)sink -
@@ -839,7 +1008,9 @@ __device__ __forceinline__ void gather_marks(const State& s, const Ctx<NT, EPW, 
     if (idx < items) {
       const int a = udiv(idx, s.mg_TW2), rem = idx - a * TW2;
       const int ti = udiv(rem, s.mg_TW), tj = rem - ti * TW;
-      const uint64_t m = gather_tile<WT>(L.fpr, row_word<WT>(s, a, 8 * ti), row_step<WT>(s), tj);
+      uint64_t m = gather_tile<WT>(L.fpr, row_word<WT>(s, a, 8 * ti), row_step<WT>(s), tj);
+      if (fan_on(s))  // the fan's column-line marks, transposed back
+        m |= transpose8(gather_tile<WT>(L.cmark, row_word<WT>(s, a, 8 * tj), row_step<WT>(s), ti));
       I.mf[k] = m & ~I.n[k];
       I.mo[k] = m & I.n[k];
       L.fp[idx] = I.mf[k];
@@ -987,10 +1158,10 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 }
 
 // sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
-template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN>
+template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
-  sense<NT, EPW, WT, SUK, KN>(s, C);
+  sense<NT, EPW, WT, SUK, KN, KM>(s, C);
   __syncthreads();
   STAMP(13);
   if (s.sensor == 0) {
@@ -1019,7 +1190,7 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32>
+template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32, int KM = 0>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -1096,7 +1267,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI, O32>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
-  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN, KM>(s, C, I);
   store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
@@ -1350,7 +1521,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   const bool valid = e_raw < s.B;  // a short last workgroup leaves a slot idle
   C.e = valid ? e_raw : s.B - 1;
   const size_t slot_lds =
-      env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, (int)sizeof(WT));
+      state_lds_bytes(s, (int)sizeof(WT));
   C.L = carve<WT>(smem + slot * slot_stride(slot_lds), s);
   const Lds<WT>& L = C.L;
   const int e = C.e;
@@ -1380,6 +1551,19 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   const int nbl = lidar ? s.nbeams : 1;  // a square env reads a dummy record
   const int4 bm0 = reinterpret_cast<const int4*>(lidar ? (const void*)s.beams : (const void*)s.pos)
       [C.sub < nbl ? C.sub : 0];
+  // fan march: the fan data (LUTs, sector and special records) instead of the
+  // beam records, up to 3 * LPE int4 in this round trip
+  const bool fan = fan_on(s);
+  const int n16 = fan ? s.fan_words / 4 : 0;
+  const int4* fsrc = reinterpret_cast<const int4*>(s.fan_data);
+  int4 fv[3];
+  if (fan) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int j = C.sub + i * LPE;
+      fv[i] = fsrc[j < n16 ? j : 0];
+    }
+  }
   zero_marks<NT, EPW, WT>(s, C);  // overlaps the round trip
   // every result is needed below: keep the compiler from sinking a load into
   // the branch that uses it (that would make it a round trip of its own)
@@ -1412,7 +1596,13 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     L.dm[C.sub] = mw.x;
     L.dw[C.sub] = mw.y;
   }
-  if (lidar) {
+  if (fan) {
+    int4* dst = reinterpret_cast<int4*>(L.fan);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (C.sub + i * LPE < n16) dst[C.sub + i * LPE] = fv[i];
+    for (int j = C.sub + 3 * LPE; j < n16; j += LPE) dst[j] = fsrc[j];
+  } else if (lidar) {
     if (C.sub < s.nbeams) reinterpret_cast<int4*>(L.beams)[C.sub] = bm0;
     for (int b = C.sub + LPE; b < s.nbeams; b += LPE) L.beams[b] = s.beams[b];
   }
@@ -1457,7 +1647,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       __syncthreads();
     }
     STAMP(3);
-    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM>(s, C, I);
     __syncthreads();
     STAMP(5);
     // every lane of the slot computes the reward and done (the same values:
@@ -1520,7 +1710,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
@@ -1529,7 +1719,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, reset_req ? inj_pos : nullptr);
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
     // obs of the current state only (dec_grid_rl.py:104-107,160)
@@ -1607,7 +1797,7 @@ template <int T, int P, typename W, class SH>
 static void launch_one(const State& s, int mode, const uint8_t* actions, const uint8_t* env_mask,
                        const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs, uint8_t* adj,
                        hipStream_t stream) {
-  const size_t slot_lds = env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, (int)sizeof(W));
+  const size_t slot_lds = state_lds_bytes(s, (int)sizeof(W));
   hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + P - 1) / P), dim3(T), slot_stride(slot_lds) * P,
                      stream, s, mode, actions, env_mask, inj_pos, reward, done, obs, adj);
 }

@@ -86,6 +86,14 @@ struct State {
   // the robot (bit 3*(dx+1) + (dy+1)); the march marks them once per agent
   // instead of once per ray (0 = no premark, the march marks step 1)
   uint32_t beam_k1;
+  // Fan march of a dense beam set (mc_env_kernel.hip fan_march; built by
+  // mc_set_beam_table, off when fan_nsec + fan_nspec == 0).  fan_data: the
+  // spread / expand LUTs (kFanLutBytes), fan_nsec sector records of
+  // fan_kt + 1 words (word 0: FAN_* class bits, word k: step k's entry) and
+  // fan_nspec special-beam records of 4 words (beam, class bits, msign, K);
+  // fan_words words in all (a multiple of 4), copied into LDS each launch.
+  int fan_nsec, fan_nspec, fan_kt, fan_words;
+  const uint32_t* fan_data;
   int32_t* env_grid;
   int32_t* pos;
   uint64_t* moved;
@@ -145,18 +153,43 @@ __host__ __device__ inline int row_plane_words(int N, int TW, int rowbytes) {
   return rowbytes == 4 ? 8 * TW * (N | 1) : N * (8 * TW + 1);
 }
 
+// Fan march (mc_env_kernel.hip fan_march): sectors of up to kFanS adjacent
+// beams of one octant class march together.  Entry of step k (u32):
+// bits 0-5 lo + 32 (signed minor offset of the sector's first cell), bits 6-10
+// D (bit j: beam j+1 sits one cell past beam j), bits 16-21 the beams still in
+// range (K >= k).  LUTs: spread[D][A] (cells lit by the live beams A) and
+// expand[D][F] (beams on the cells F), 2048 bytes each.
+constexpr int kFanS = 6;
+constexpr int kFanLutBytes = 4096;
+enum : uint32_t { FAN_COLS = 1u, FAN_NEG = 2u };  // class bits: major axis y (a column line); major sign -1
+
+// LDS bytes of the fan region (replaces the beam records): column planes
+// neg / marks / seen, the fan data and the per-(agent, special beam) entries
+__host__ __device__ inline size_t fan_lds_bytes(int N, int TW, int rowbytes, int nspec, int kt, int words) {
+  return ((((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15) +
+         (size_t)words * 4 + (size_t)N * nspec * (kt + 1) * 4;
+}
+
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
-// rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.
-__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes) {
+// rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.  fanb: the
+// fan region's bytes (0: beam records instead).
+__host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes, size_t fanb = 0) {
   // fold, oold, fp tiles; the square sensor (nbeams == 0) also neg, pos, op
   size_t b = (size_t)(nbeams > 0 ? 3 : 6) * N * TW * TW * 8;
   b += (((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
-  b += (size_t)(nbeams > 0 ? nbeams : 1) * 16;         // beams
+  b += fanb ? ((fanb + 15) & ~(size_t)15) : (size_t)(nbeams > 0 ? nbeams : 1) * 16;  // fan region / beams
   b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
   b += 64;                                             // scalars
   b += ((size_t)N + 15) & ~(size_t)15;                 // actions
   b += 64 * (size_t)rowbytes;                          // per-lane sink words (lidar marks)
   return b;
+}
+
+// the env slot of a State (lidar beams or fan region)
+__host__ __device__ inline size_t state_lds_bytes(const State& s, int rowbytes) {
+  const bool fan = s.sensor == 0 && s.fan_nsec + s.fan_nspec > 0;
+  return env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, rowbytes,
+                       fan ? fan_lds_bytes(s.N, s.TW, rowbytes, s.fan_nspec, s.fan_kt, s.fan_words) : 0);
 }
 
 // Byte stride between the env slots of a workgroup: skewed by 20 LDS banks so

@@ -3,6 +3,7 @@ oracle and the reference's golden vectors.  Bit-exact on masks, positions,
 obs, done and counters; rewards compared exactly (tolerance 0: every reward
 term is an integer-valued or config-valued float64 added in reference order,
 well inside north_star's 1e-6)."""
+import os
 import zlib
 
 import numpy as np
@@ -116,6 +117,17 @@ BATCH_CASES = {
                          lambda rs: bern(rs, 40, 40, 0.1), 2, 12),
     "limit_range27_ego15": (base_cfg(numrobot=4, egoradius=15, sensor_config={"num_lasers": 13, "range": 27}),
                             lambda rs: bern(rs, 90, 70, 0.1), 2, 10),
+    # dense beam sets: the fan march (sectors of adjacent beams, mc_env_kernel
+    # fan_march) on 64-bit rows with special beams, without special beams at
+    # range 27, and on 32-bit rows (window of 3 x 3 tiles)
+    "fan_128beams_r13_nonsquare": (base_cfg(numrobot=3, allow_even_beams=True,
+                                            sensor_config={"num_lasers": 128, "range": 13.5}),
+                                   lambda rs: bern(rs, 60, 90, 0.12), 6, 25),
+    "fan_361beams_r27": (base_cfg(numrobot=2, sensor_config={"num_lasers": 361, "range": 27}),
+                         lambda rs: bern(rs, 80, 80, 0.08), 3, 10),
+    "fan_100beams_r6_u32": (base_cfg(numrobot=3, allow_even_beams=True,
+                                     sensor_config={"num_lasers": 100, "range": 6}),
+                            lambda rs: bern(rs, 40, 40, 0.15), 6, 30),
     # dijkstra_input obs layer: BFS path to the nearest
     # unexplored cell; long episodes on small grids reach long paths
     "dijkstra_square_r1": (base_cfg(numrobot=2, dijkstra_input=1, sensor_type="square_sensor",
@@ -177,6 +189,12 @@ BATCH_CASES = {
 }
 
 
+# dense beam sets: the lidar marches by sectors (fan_march) unless
+# MARLCOV_FAN=0 / MARLCOV_BEAM_TABLE keep the ray march
+FAN_CASES = sorted([n for n in BATCH_CASES if n.startswith("fan_")] +
+                   ["c4_like_n8_256_360beams", "lidar360_single_tool"])
+
+
 @pytest.mark.parametrize("name", sorted(BATCH_CASES))
 def test_batch_matches_oracle(torch_cuda, name):
     import marlcov
@@ -192,6 +210,9 @@ def test_batch_matches_oracle(torch_cuda, name):
         refs.append(r)
         pos.append(np.stack([r._xinds, r._yinds], 1))
     env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False, want_adjacency=True)
+    if name in FAN_CASES:
+        want = os.environ.get("MARLCOV_FAN") != "0" and "MARLCOV_BEAM_TABLE" not in os.environ
+        assert ("+fan(" in env.kernel_variant()) == want, env.kernel_variant()
     obs, adj = env.reset(positions=np.stack(pos))
     st = device_state(env)
     obs_h = full_obs(env, obs, cfg)
@@ -408,6 +429,14 @@ def test_batch_matches_oracle_full_beam_table(torch_cuda, name, monkeypatch):
     otherwise uses each beam's common step bits when the host proves them
     equivalent: mc_set_beam_table, State::beam_common)."""
     monkeypatch.setenv("MARLCOV_BEAM_TABLE", "1")
+    test_batch_matches_oracle(torch_cuda, name)
+
+
+@pytest.mark.parametrize("name", FAN_CASES)
+def test_batch_matches_oracle_ray_march(torch_cuda, name, monkeypatch):
+    """The dense cases with the ray march (MARLCOV_FAN=0) instead of the
+    sector march."""
+    monkeypatch.setenv("MARLCOV_FAN", "0")
     test_batch_matches_oracle(torch_cuda, name)
 
 

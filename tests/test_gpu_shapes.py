@@ -105,19 +105,27 @@ def test_compiled_shape_auto_reset(torch_cuda, name):
     assert resets >= B  # maxsteps=7 over >= 20 steps: every env reset at least twice, less sentinels
 
 
-def test_c4_shape_256_many_envs(torch_cuda):
+@pytest.mark.parametrize("march", ["fan", "rays"])
+def test_c4_shape_256_many_envs(torch_cuda, monkeypatch, march):
     """BASELINE configs[3] geometry (8 agents, 256x256, 360 beams, R=20) on
     16 envs x 40 steps through the C4 instantiation, with auto-resets (maxsteps
-    13).  360 beams never share one step pattern over every start (mc_set_beam_table:
-    beam_common is off), so the march reads the per-start beam table."""
+    13).  358 of the 360 beams share one step pattern over every start and
+    march in 64 sectors (fan_march); 270 and 315 degrees march as special
+    one-beam sectors from their per-start patterns.  "rays": the ray march
+    (MARLCOV_FAN=0)."""
     import marlcov
     torch = torch_cuda
+    if march == "rays":
+        monkeypatch.setenv("MARLCOV_FAN", "0")
+    else:
+        monkeypatch.delenv("MARLCOV_FAN", raising=False)
     cfg = base_cfg(numrobot=8, maxsteps=13, allow_even_beams=True, sensor_config={"num_lasers": 360, "range": 20})
     rs = np.random.RandomState(404)
     B = 16
     grids = [bern(rs, 256, 256, 0.1) for _ in range(B)]
     env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=True, seed=5)
     assert ",C4>" in env.kernel_variant(), env.kernel_variant()
+    assert ("+fan(64/2)" in env.kernel_variant()) == (march == "fan"), env.kernel_variant()
     env.reset()
     resets = run_against_oracle(torch, env, cfg, rs, 40, list(range(B)), 5, "c4_256", sentinel_p=0.02)
     assert resets >= B
