@@ -434,17 +434,19 @@ int mc_query(void* env, mc_layout* out) {
 }
 
 // Fan march data of a dense beam set (mc_env_kernel.hip fan_march, layout in
-// mc_internal.h State::fan_data).  The beams with one step pattern for every
-// start are grouped by octant class (major axis, major sign, minor sign;
-// minor sign 0 counts as +), ordered by their minor offsets, and cut greedily
-// into sectors of up to kFanS beams whose offsets differ by 0 or 1 between
-// neighbours at every step; the classes are interleaved, so the sectors of
-// one march instruction mark different lines.  Beams with start-dependent
-// patterns (Beam::axis bit 1) become one-beam special sectors.  Returns false
-// (ray march) for sparse sets: fewer than 64 beams (dense_beams), or fewer
-// than two beams per sector on average.
-static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lanes,
-                      std::vector<uint32_t>& out, int& nsec, int& nspec) {
+// mc_internal.h State::fan_data).  Beams are grouped by octant class (major
+// axis, major sign, minor sign; minor sign 0 counts as +), ordered by their
+// minor offsets, and cut greedily into sectors of up to kFanS beams whose
+// offsets differ by 0 or 1 between neighbours at every step, at most one
+// start-dependent beam (Beam::axis bit 1) per sector; the classes are
+// interleaved, so the sectors of one march instruction mark different lines.
+// A start-dependent beam marches with its common bits except from the minor
+// starts where its own bits differ before the march ends (bits[b][start],
+// cm starts); the kernel marches those alone.  Returns false (ray march) for
+// sparse sets: fewer than 64 beams (dense_beams), or fewer than two beams per
+// sector on average.
+static bool build_fan(const std::vector<mc::Beam>& bt, const std::vector<uint64_t>& bits, int cmax, int Wp,
+                      int Lp, int kmax, int N, int lanes, std::vector<uint32_t>& out, int& nsec, int& nspec) {
   const int nb = (int)bt.size();
   if (nb < 64 || kmax > 27) return false;
   auto off = [](const mc::Beam& o, int k) {  // signed minor offset of step k
@@ -454,7 +456,7 @@ static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lane
   std::vector<int> spec;
   for (int b = 0; b < nb; ++b) {
     const mc::Beam& o = bt[b];
-    if (o.axis & 2) { spec.push_back(b); continue; }
+    if (o.axis & 2) spec.push_back(b);
     cls[(o.axis & 1) * 4 + (o.sign < 0 ? 2 : 0) + (o.msign < 0 ? 1 : 0)].push_back(b);
   }
   std::vector<std::vector<std::vector<int>>> secs(8);
@@ -471,6 +473,8 @@ static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lane
     for (int b : v) {
       std::vector<std::vector<int>>& S = secs[c];
       bool join = !S.empty() && (int)S.back().size() < mc::kFanS;
+      if (join && (bt[b].axis & 2))
+        for (int o : S.back()) join = join && !(bt[o].axis & 2);
       for (int k = 1; join && k <= kmax; ++k) {
         const int d = off(bt[b], k) - off(bt[S.back().back()], k);
         join = d == 0 || d == 1;
@@ -486,7 +490,7 @@ static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lane
       if (i < secs[c].size()) order.push_back(&secs[c][i]);
   nsec = (int)order.size();
   nspec = (int)spec.size();
-  if (2 * (nsec + nspec) > nb || N * nspec > lanes) return false;
+  if (2 * nsec > nb || N * nspec > lanes || nspec > 255) return false;
   out.assign(mc::kFanLutBytes / 4, 0u);
   uint8_t* lut = reinterpret_cast<uint8_t*>(out.data());
   for (int D = 0; D < 32; ++D) {
@@ -507,7 +511,13 @@ static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lane
   };
   for (const std::vector<int>* S : order) {
     const std::vector<int>& v = *S;
-    out.push_back(cbits(bt[v[0]]));
+    uint32_t w0 = cbits(bt[v[0]]);
+    for (size_t j = 0; j < v.size(); ++j)
+      if (bt[v[j]].axis & 2) {
+        const size_t si = std::find(spec.begin(), spec.end(), v[j]) - spec.begin();
+        w0 |= mc::FAN_SPECIAL | ((uint32_t)j << 3) | ((uint32_t)si << 8);
+      }
+    out.push_back(w0);
     for (int k = 1; k <= kmax; ++k) {
       const int lo = off(bt[v[0]], k);
       uint32_t D = 0, valid = 0;
@@ -519,10 +529,24 @@ static bool build_fan(const std::vector<mc::Beam>& bt, int kmax, int N, int lane
     }
   }
   for (int b : spec) {
-    out.push_back((uint32_t)b);
-    out.push_back(cbits(bt[b]));
-    out.push_back((uint32_t)bt[b].msign);
-    out.push_back((uint32_t)bt[b].K);
+    // the starts whose own bits leave the common path before the march ends
+    // (the check of mc_set_beam_table's common-pattern test)
+    const mc::Beam& o = bt[b];
+    const int cm = (o.axis & 1) == 0 ? Lp : Wp;
+    const uint64_t* row = &bits[(size_t)b * cmax];
+    int elo = 1 << 30, ehi = -1;
+    for (int c0 = 1; c0 + 1 < cm; ++c0) {
+      int p = c0, c = c0;
+      for (int k = 0; k < o.K; ++k) {
+        p += ((row[c0] >> k) & 1) ? o.msign : 0;
+        c += ((o.bits >> k) & 1) ? o.msign : 0;
+        if (p != c) { elo = std::min(elo, c0); ehi = std::max(ehi, c0); break; }
+        if (p <= 0 || p >= cm - 1) break;
+      }
+    }
+    const uint32_t rec[8] = {(uint32_t)b, cbits(o), (uint32_t)o.msign, (uint32_t)o.K,
+                             (uint32_t)elo, (uint32_t)ehi, 0u, 0u};
+    out.insert(out.end(), rec, rec + 8);
   }
   while (out.size() % 4) out.push_back(0u);
   return true;
@@ -663,7 +687,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     int nsec = 0, nspec = 0;
     const char* fv = getenv("MARLCOV_FAN");
     bool on = !getenv("MARLCOV_BEAM_TABLE") && !(fv && fv[0] == '0') &&
-              build_fan(bt, kmax, E->s.N, E->nt / E->epw, fd, nsec, nspec);
+              build_fan(bt, bits, cmax, E->s.Wp, E->s.Lp, kmax, E->s.N, E->nt / E->epw, fd, nsec, nspec);
     const int rb = E->s.TW <= 4 ? 4 : 8;
     if (on && mc::env_lds_bytes(E->s.N, E->s.TW, num_beams, rb,
                                 mc::fan_lds_bytes(E->s.N, E->s.TW, rb, nspec, kmax, (int)fd.size())) > 65536)

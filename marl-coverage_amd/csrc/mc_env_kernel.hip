@@ -771,24 +771,27 @@ __device__ __forceinline__ bool ray_mark(const Lds<WT>& L, Ray& R, int k, WT nro
 }
 
 // --------------------------------------------------------------------------
-// Fan march: dense beam sets (lidar.py:34-63).  Every beam whose step bits
-// are the same from every start (Beam::axis bit 1 clear) belongs to an octant
-// class (major axis and sign; mc_set_beam_table) and all of a class's beams
-// sit on the same line at step k: the row (or column) k cells from the robot.
-// A sector is up to kFanS beams of one class, ordered by minor offset, that
-// are never more than one cell apart at any step, so at step k its beams
-// cover the cells lo(k) .. lo(k) + 5 of the line and the beam -> cell map is
-// the monotone map D(k).  A lane marches one (agent, sector) with the live
-// beams A as bits: the cells lit at step k are spread[D][A] (each is marked:
-// free up to the first obstacle, and that obstacle), and the beams whose cell
-// is an obstacle, expand[D][F], leave A.  One step is a few bit operations
-// and three LUT / table reads for up to six beams, where the ray march spends
-// a dozen VALU operations per ray and step.  Beams with start-dependent bits
-// (C4: 270 and 315 degrees) march as one-beam sectors whose entries the lane
-// builds from the start word of its robot's post-move cell.  Column lines read
-// and mark the column planes (cneg / cmark / cseen), which the stage fills
-// with transposed tiles and gather_marks transposes back.  Cells the agent has
-// seen (cseen / fldr) are not marked again (dense_beams).
+// Fan march: dense beam sets (lidar.py:34-63).  Every beam belongs to an
+// octant class (major axis and sign, minor sign; mc_set_beam_table) and all of
+// a class's beams sit on the same line at step k: the row (or column) k cells
+// from the robot.  A sector is up to kFanS beams of one class, ordered by
+// minor offset, that are never more than one cell apart at any step, so at
+// step k its beams cover the cells lo(k) .. lo(k) + 5 of the line and the
+// beam -> cell map is the monotone map D(k).  A lane marches one (agent,
+// sector) with the live beams A as bits: the cells lit at step k are
+// spread[D][A] (each is marked: free up to the first obstacle, and that
+// obstacle), and the beams whose cell is an obstacle, expand[D][F], leave A.
+// One step is a few bit operations and three LUT / table reads for up to six
+// beams, where the ray march spends a dozen VALU operations per ray and step.
+// A beam whose step bits depend on the start coordinate (Beam::axis bit 1;
+// C4: 270 and 315 degrees, for minor starts 1..3) marches in its sector with
+// its common bits unless its robot's start lies in the beam's exceptional
+// range; then the sector leaves it out and the lane marches it alone, from
+// the start's own bits, after the sectors (a pass only waves with such a
+// robot take).  Column lines read and mark the column planes (cneg / cmark /
+// cseen), which the stage fills with transposed tiles and gather_marks
+// transposes back.  Cells the agent has seen (cseen / fldr) are not marked
+// again (dense_beams).
 // --------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const lds_char*)(const char*)p;
@@ -798,93 +801,103 @@ __device__ __forceinline__ T* lds_ptr(uint32_t a) {
   return reinterpret_cast<T*>((char*)((lds_char*)(uintptr_t)a));
 }
 
+// one (agent, sector): entries T[1..kt] (T[0]: class bits), live beams A
+template <typename WT, int KM>
+__device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, const uint32_t* T, int a,
+                                           uint32_t A, int kt) {
+  constexpr int SU = 5;  // steps per batch: reads, then the live-beam chain, then marks
+  const uint32_t MD = (uint32_t)(row_plane_words(s.N, s.TW, (int)sizeof(WT)) * (int)sizeof(WT));  // neg -> marks
+  const uint8_t* spread = reinterpret_cast<const uint8_t*>(L.fan);
+  const uint8_t* expand = spread + 2048;
+  const uint32_t desc = T[0];
+  const bool cols = (desc & FAN_COLS) != 0;
+  const int lx = L.x[a] - 8 * L.bx[a], ly = L.y[a] - 8 * L.by[a];
+  // the line's word in the neg plane (row lx + sign k, or column ly + sign k);
+  // marks MD bytes on, seen cells 2 MD on
+  const uint32_t P0 = lds_addr(cols ? L.cneg : L.negr) + (uint32_t)row_word<WT>(s, a, cols ? ly : lx) * sizeof(WT);
+  const int stride = ((desc & FAN_NEG) ? -1 : 1) * row_step<WT>(s) * (int)sizeof(WT);
+  const int bb = (cols ? lx : ly) - 32;  // bit of the cell at minor offset lo: bb + (lo + 32)
+  for (int k0 = 1; k0 <= kt; k0 += SU) {
+    uint32_t e[SU], F[SU], SN[SU], kill[SU], lit[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      e[u] = F[u] = SN[u] = 0;
+      if (KM > 0 ? (k0 + u <= KM) : (k0 + u <= kt)) {
+        e[u] = T[k0 + u];
+        const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
+        const int sh = bb + (int)(e[u] & 63u);
+        F[u] = (uint32_t)(*lds_ptr<const WT>(P) >> sh) & 63u;
+        SN[u] = (uint32_t)(*lds_ptr<const WT>(P + 2 * MD) >> sh) & 63u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) kill[u] = expand[(e[u] & 0x7C0u) | F[u]];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      A &= e[u] >> 16;  // in range (a step past the trip count has e = 0)
+      lit[u] = spread[(e[u] & 0x7C0u) | A];
+      A &= ~kill[u];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const uint32_t nm = lit[u] & ~SN[u];
+      if (nm) {
+        const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
+        lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)(e[u] & 63u)));
+      }
+    }
+  }
+}
+
 template <int NT, int EPW, typename WT, int KM>
 __device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
-  constexpr int SU = 5;  // steps per batch: reads, then the live-beam chain, then marks
   const Lds<WT>& L = C.L;
   const int N = s.N;
   const int kt = KM > 0 ? KM : s.fan_kt;
   const int nsec = s.fan_nsec, nspec = s.fan_nspec;
-  const int qs = N * nsec;  // first special lane-sector
-  const int total = qs + N * nspec;
-  const uint32_t MD = (uint32_t)(row_plane_words(N, s.TW, (int)sizeof(WT)) * (int)sizeof(WT));  // neg -> marks
-  const uint32_t lut = lds_addr(L.fan);  // spread at lut, expand at lut + 2048
+  const int qs = N * nsec;  // (agent, sector) lane-sectors
   const uint32_t* sec = L.fan + kFanLutBytes / 4;
-  const uint32_t* sdesc = sec + nsec * (kt + 1);
-  // the lane that marches special i (lane-sector qs + i; mc_set_beam_table
-  // keeps N * nspec <= lanes per env, one per lane) loads the start word of
-  // its robot's post-move cell now, for a later pass
+  const uint32_t* sdesc = sec + nsec * (kt + 1);  // special beams: 8 words each
+  // special beam i of (agent, special) pairs: lane (qs + i) % LPE
+  // (mc_set_beam_table keeps N * nspec <= lanes per env) loads the start word
+  // of its robot's post-move cell now, for the pass after the sectors
   uint32_t spw = 0;
-  if (nspec > 0) {
-    int i = C.sub - qs % LPE;
-    if (i < 0) i += LPE;
-    if (i < N * nspec) {
-      const int a = i / nspec, j = i - a * nspec;
-      const uint32_t* d = sdesc + 4 * j;
-      const int c0 = (d[1] & FAN_COLS) ? L.x[a] : L.y[a];  // the minor coordinate
-      spw = (uint32_t)s.beam_bits[(size_t)d[0] * s.bcmax + c0];
-    }
+  bool exc = false;
+  int si = C.sub - qs % LPE;
+  if (si < 0) si += LPE;
+  if (nspec > 0 && si < N * nspec) {
+    const int a = si / nspec;
+    const uint32_t* d = sdesc + 8 * (si - a * nspec);
+    const int c0 = (d[1] & FAN_COLS) ? L.x[a] : L.y[a];  // the minor coordinate
+    exc = c0 >= (int)d[4] && c0 <= (int)d[5];
+    if (exc) spw = (uint32_t)s.beam_bits[(size_t)d[0] * s.bcmax + c0];
   }
-  for (int q = C.sub; q < total; q += LPE) {
-    int a;
-    const uint32_t* T;
-    if (q < qs) {
-      const int sg = q / N;
-      a = q - sg * N;
-      T = sec + sg * (kt + 1);
-    } else {  // special beam: a one-beam sector (D = 0) with this start's steps
-      const int i = q - qs;
-      a = i / nspec;
-      const uint32_t* d = sdesc + 4 * (i - a * nspec);
+  for (int q = C.sub; q < qs; q += LPE) {
+    const int sg = q / N, a = q - sg * N;
+    const uint32_t* T = sec + sg * (kt + 1);
+    const uint32_t desc = T[0];
+    uint32_t A = 63u;
+    if (desc & FAN_SPECIAL) {  // the sector's special beam: left out from an exceptional start
+      const uint32_t* d = sdesc + 8 * (desc >> 8);
+      const int c0 = (desc & FAN_COLS) ? L.x[a] : L.y[a];
+      if (c0 >= (int)d[4] && c0 <= (int)d[5]) A &= ~(1u << ((desc >> 3) & 7u));
+    }
+    fan_sector<WT, KM>(s, L, T, a, A, kt);
+  }
+  if (__ballot(exc)) {  // one-beam march of the left-out beams, from the start's bits
+    if (exc) {
+      const int a = si / nspec;
+      const uint32_t* d = sdesc + 8 * (si - a * nspec);
       const int msign = (int)d[2], K = (int)d[3];
-      uint32_t* W = L.fspec + i * (kt + 1);
+      uint32_t* W = L.fspec + si * (kt + 1);
       W[0] = d[1];
       int lo = 0;
       for (int k = 1; k <= kt; ++k) {
         lo += ((spw >> (k - 1)) & 1u) ? msign : 0;
         W[k] = (uint32_t)(lo + 32) | (K >= k ? (1u << 16) : 0u);
       }
-      T = W;
-    }
-    const uint32_t desc = T[0];
-    const bool cols = (desc & FAN_COLS) != 0;
-    const int lx = L.x[a] - 8 * L.bx[a], ly = L.y[a] - 8 * L.by[a];
-    // the line's word in the neg plane (row lx + sign k, or column ly + sign k);
-    // marks MD bytes on, seen cells 2 MD on
-    const uint32_t P0 = lds_addr(cols ? L.cneg : L.negr) + (uint32_t)row_word<WT>(s, a, cols ? ly : lx) * sizeof(WT);
-    const int stride = ((desc & FAN_NEG) ? -1 : 1) * row_step<WT>(s) * (int)sizeof(WT);
-    const int bb = (cols ? lx : ly) - 32;  // bit of the cell at minor offset lo: bb + (lo + 32)
-    uint32_t A = 63u;
-    for (int k0 = 1; k0 <= kt; k0 += SU) {
-      uint32_t e[SU], F[SU], SN[SU], kill[SU], lit[SU];
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        e[u] = F[u] = SN[u] = 0;
-        if (KM > 0 ? (k0 + u <= KM) : (k0 + u <= kt)) {
-          e[u] = T[k0 + u];
-          const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-          const int sh = bb + (int)(e[u] & 63u);
-          F[u] = (uint32_t)(*lds_ptr<const WT>(P) >> sh) & 63u;
-          SN[u] = (uint32_t)(*lds_ptr<const WT>(P + 2 * MD) >> sh) & 63u;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < SU; ++u) kill[u] = *lds_ptr<const uint8_t>(lut + 2048 + ((e[u] & 0x7C0u) | F[u]));
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        A &= e[u] >> 16;  // in range (a step past the trip count has e = 0)
-        lit[u] = *lds_ptr<const uint8_t>(lut + ((e[u] & 0x7C0u) | A));
-        A &= ~kill[u];
-      }
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        const uint32_t nm = lit[u] & ~SN[u];
-        if (nm) {
-          const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-          lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)(e[u] & 63u)));
-        }
-      }
+      fan_sector<WT, KM>(s, L, W, a, 1u, kt);
     }
   }
 }

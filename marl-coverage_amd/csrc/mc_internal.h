@@ -90,7 +90,7 @@ struct State {
   // mc_set_beam_table, off when fan_nsec + fan_nspec == 0).  fan_data: the
   // spread / expand LUTs (kFanLutBytes), fan_nsec sector records of
   // fan_kt + 1 words (word 0: FAN_* class bits, word k: step k's entry) and
-  // fan_nspec special-beam records of 4 words (beam, class bits, msign, K);
+  // fan_nspec special-beam records of 8 words (FAN_SPECIAL);
   // fan_words words in all (a multiple of 4), copied into LDS each launch.
   int fan_nsec, fan_nspec, fan_kt, fan_words;
   const uint32_t* fan_data;
@@ -161,7 +161,12 @@ __host__ __device__ inline int row_plane_words(int N, int TW, int rowbytes) {
 // expand[D][F] (beams on the cells F), 2048 bytes each.
 constexpr int kFanS = 6;
 constexpr int kFanLutBytes = 4096;
-enum : uint32_t { FAN_COLS = 1u, FAN_NEG = 2u };  // class bits: major axis y (a column line); major sign -1
+// Sector record word 0: FAN_COLS (major axis y: a column line), FAN_NEG
+// (major sign -1), FAN_SPECIAL (the sector holds a beam with start-dependent
+// bits: its slot in bits 3-5, its special record in bits 8+).  Special
+// record (8 words): beam, class bits, minor sign, K, first and last minor
+// start whose bits differ from the common ones.
+enum : uint32_t { FAN_COLS = 1u, FAN_NEG = 2u, FAN_SPECIAL = 4u };
 
 // LDS bytes of the fan region (replaces the beam records): column planes
 // neg / marks / seen, the fan data and the per-(agent, special beam) entries

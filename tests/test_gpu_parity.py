@@ -432,6 +432,50 @@ def test_batch_matches_oracle_full_beam_table(torch_cuda, name, monkeypatch):
     test_batch_matches_oracle(torch_cuda, name)
 
 
+def test_fan_exceptional_starts(torch_cuda):
+    """360 beams: 270 and 315 degrees leave their common step pattern from the
+    minor starts x = 1..3 (mc_set_beam_table), where the sector march leaves
+    them out and marches them alone from the start's own bits.  Robots start
+    on rows 1..3 and near the other borders; every step is compared."""
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=4, allow_even_beams=True, sensor_config={"num_lasers": 360, "range": 8})
+    rs = np.random.RandomState(360)
+    B, N, T = 8, 4, 16
+    grids = [bern(rs, 30, 34, 0.1) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False)
+    assert "+fan(" in env.kernel_variant(), env.kernel_variant()
+    pos = np.zeros((B, N, 2), np.int32)
+    refs = []
+    for b in range(B):
+        g = np.pad(grids[b], 1, constant_values=-1)
+        cells = []
+        for x in [1 + b % 3, 2, 3, 30 - b % 3]:  # padded rows 1..3 (exceptional) and the far border
+            free = [y for y in range(1, g.shape[1] - 1) if g[x, y] >= 0 and (x, y) not in cells]
+            cells.append((x, free[rs.randint(len(free))]))
+        pos[b] = cells
+        np.random.seed(b)
+        r = DecGridRLRef([grids[b]], cfg)
+        r.reset(False, None, positions=cells)
+        refs.append(r)
+    obs = env.reset(positions=pos)
+    st = device_state(env)
+    for b in range(B):
+        compare_env(st, b, refs[b], f"reset env {b}")
+    for t in range(T):
+        acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h = full_obs(env, obs, cfg), rew.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"t={t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+    env.check()
+
+
 @pytest.mark.parametrize("name", FAN_CASES)
 def test_batch_matches_oracle_ray_march(torch_cuda, name, monkeypatch):
     """The dense cases with the ray march (MARLCOV_FAN=0) instead of the
