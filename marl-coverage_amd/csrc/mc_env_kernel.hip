@@ -281,7 +281,7 @@ __device__ __forceinline__ int pick(const int (&R)[NS], int a) {
 // lane indices (v_readlane) and selected by slot
 template <int NT, int EPW, typename WT>
 __device__ __forceinline__ int slot_lane(const Ctx<NT, EPW, WT>& C, int v, int i) {
-  static_assert(NT == 64, "one wave per workgroup");
+  static_assert(NT == 64 || EPW == 1, "one wave per workgroup, or the first wave of one env");
   if constexpr (EPW == 1) return rdlane(v, i);
   else {
     static_assert(EPW == 2, "two slots per wave");
@@ -1523,6 +1523,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   // register front (front_regs / moves_front): compiled agent count <= 8,
   // one wave per workgroup
   constexpr bool FRONT = NSM > 0 && NT == 64;
+  // moves from registers in the first wave of a multi-wave env during round
+  // trip 2 (compiled agent count <= 8, lidar: C4)
+  constexpr bool EARLY = NSM > 0 && NT > 64 && EPW == 1 && SH::NB > 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int N = s.N;
@@ -1639,6 +1642,24 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       moves_front<NT, EPW, WT, NSM>(s, C, F, !inb || ((tt >> tile_bit(tx, ty)) & 1ull),
                                     (uint32_t)tx | ((uint32_t)ty << 16), act, moved0, -s.pen);
       stage_scatter<NT, EPW, WT, KI>(s, C, I);
+    } else if constexpr (EARLY) {
+      // ---- round trip 2 with the moves of a multi-wave env: the first wave
+      // moves the robots from registers (front_regs / moves_front: lane i
+      // holds robot i, its target-cell grid tile loaded first) while the
+      // staged tiles are in flight; the other waves only stage
+      const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+      const int tx = p0.x + dx, ty = p0.y + dy;
+      const bool inb = (unsigned)tx < (unsigned)s.Wp && (unsigned)ty < (unsigned)s.Lp;
+      const uint64_t tt = ld_tile<O32>(s.grid_neg, __umul24((uint32_t)g0, (uint32_t)s.MT) +
+                                                       tile_index24(s.TCS, inb ? tx >> 3 : 0, inb ? ty >> 3 : 0));
+      stage_load<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
+      if (C.sub < 64) {
+        Front<NSM> F;
+        front_regs<NT, EPW, WT, NSM>(s, C, p0.x, p0.y, act, F);
+        moves_front<NT, EPW, WT, NSM>(s, C, F, !inb || ((tt >> tile_bit(tx, ty)) & 1ull),
+                                      (uint32_t)tx | ((uint32_t)ty << 16), act, moved0, -s.pen);
+      }
+      stage_scatter<NT, EPW, WT, KI>(s, C, I);
     } else {
       stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);  // ---- round trip 2 ----
     }
@@ -1649,7 +1670,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     STAMP(2);
     // (the same loop on the scalar unit, robots read by v_readlane, was
     // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
-    if constexpr (!FRONT) {  // (FRONT: moved during round trip 2)
+    if constexpr (!FRONT && !EARLY) {  // (FRONT, EARLY: moved during round trip 2)
       // the first wave of the slot moves the robots (lane 0 publishes); the
       // other waves of a multi-wave workgroup only wait at the barrier
       if constexpr (SH::N > 0 && SH::N <= 8) {
