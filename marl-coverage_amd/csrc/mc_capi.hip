@@ -690,7 +690,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
               build_fan(bt, bits, cmax, E->s.Wp, E->s.Lp, kmax, E->s.N, E->nt / E->epw, fd, nsec, nspec);
     const int rb = E->s.TW <= 4 ? 4 : 8;
     if (on && mc::env_lds_bytes(E->s.N, E->s.TW, num_beams, rb,
-                                mc::fan_lds_bytes(E->s.N, E->s.TW, rb, nspec, kmax, (int)fd.size())) > 65536)
+                                mc::fan_lds_bytes(E->s.N, nspec, kmax, (int)fd.size())) > 65536)
       on = false;
     if (on) {
       if (fd.size() > E->fan_cap) {

@@ -101,27 +101,37 @@ __device__ __forceinline__ Lds<WT> carve(char* smem, const State& s) {
   // the grid tile planes (neg, pos) and the obstacle-mark plane (op) serve
   // the square sensor only: a lidar slot carves fold, oold, fp (env_lds_bytes)
   const bool square = s.sensor != 0;
-  L.fold = p;
-  L.oold = p + tiles;
-  L.fp = p + 2 * tiles;
+  const bool fan = fan_on(s);
+  const size_t rowplanes = (((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15;
+  // fan: the column planes overlay the tile planes -- cneg / cseen are dead
+  // after the march, cmark (read by gather_marks, which writes fp) lies past
+  // fp (rows * sizeof(WT) >= tiles * 8: TW <= 8) and under fold / oold,
+  // which the merge writes after gather_marks
+  L.fp = fan ? p : p + 2 * tiles;
+  L.fold = fan ? p + tiles : p;
+  L.oold = fan ? p + 2 * tiles : p + tiles;
   L.neg = square ? p + 3 * tiles : nullptr;
   L.pos = square ? p + 4 * tiles : nullptr;
   L.op = square ? p + 5 * tiles : nullptr;
-  char* q = smem + (size_t)(square ? 6 : 3) * tiles * 8;
+  L.cneg = L.cmark = L.cseen = nullptr;
+  if (fan) {
+    L.cneg = reinterpret_cast<WT*>(smem);
+    L.cmark = L.cneg + rows;
+    L.cseen = L.cmark + rows;
+  }
+  size_t tb = (size_t)(square ? 6 : 3) * tiles * 8;
+  if (fan && tb < rowplanes) tb = rowplanes;
+  char* q = smem + tb;
   L.negr = reinterpret_cast<WT*>(q);
   L.fpr = L.negr + rows;
   L.fldr = L.fpr + rows;
-  q += (((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15;
-  L.cneg = L.cmark = L.cseen = nullptr;
+  q += rowplanes;
   L.fan = L.fspec = nullptr;
   L.beams = reinterpret_cast<Beam*>(q);
-  if (fan_on(s)) {
-    L.cneg = reinterpret_cast<WT*>(q);
-    L.cmark = L.cneg + rows;
-    L.cseen = L.cmark + rows;
-    L.fan = reinterpret_cast<uint32_t*>(q + ((((size_t)3 * rows * sizeof(WT)) + 15) & ~(size_t)15));
+  if (fan) {
+    L.fan = reinterpret_cast<uint32_t*>(q);
     L.fspec = L.fan + s.fan_words;
-    q += (fan_lds_bytes(s.N, s.TW, (int)sizeof(WT), s.fan_nspec, s.fan_kt, s.fan_words) + 15) & ~(size_t)15;
+    q += (fan_lds_bytes(s.N, s.fan_nspec, s.fan_kt, s.fan_words) + 15) & ~(size_t)15;
   } else {
     q += (size_t)(s.nbeams > 0 ? s.nbeams : 1) * 16;
   }
@@ -805,7 +815,7 @@ __device__ __forceinline__ T* lds_ptr(uint32_t a) {
 template <typename WT, int KM>
 __device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, const uint32_t* T, int a,
                                            uint32_t A, int kt) {
-  constexpr int SU = 5;  // steps per batch: reads, then the live-beam chain, then marks
+  constexpr int SU = 10;  // steps per batch: reads, then the live-beam chain, then marks
   const uint32_t MD = (uint32_t)(row_plane_words(s.N, s.TW, (int)sizeof(WT)) * (int)sizeof(WT));  // neg -> marks
   const uint8_t* spread = reinterpret_cast<const uint8_t*>(L.fan);
   const uint8_t* expand = spread + 2048;

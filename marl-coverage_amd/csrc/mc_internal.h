@@ -168,20 +168,23 @@ constexpr int kFanLutBytes = 4096;
 // start whose bits differ from the common ones.
 enum : uint32_t { FAN_COLS = 1u, FAN_NEG = 2u, FAN_SPECIAL = 4u };
 
-// LDS bytes of the fan region (replaces the beam records): column planes
-// neg / marks / seen, the fan data and the per-(agent, special beam) entries
-__host__ __device__ inline size_t fan_lds_bytes(int N, int TW, int rowbytes, int nspec, int kt, int words) {
-  return ((((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15) +
-         (size_t)words * 4 + (size_t)N * nspec * (kt + 1) * 4;
+// LDS bytes of the fan region (replaces the beam records): the fan data and
+// the per-(agent, special beam) entries.  The fan's column planes share the
+// tile region (env_lds_bytes; mc_env_kernel.hip carve).
+__host__ __device__ inline size_t fan_lds_bytes(int N, int nspec, int kt, int words) {
+  return (size_t)words * 4 + (size_t)N * nspec * (kt + 1) * 4;
 }
 
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).
 // rowbytes: 4 when a window row (8*TW cells) fits a u32, else 8.  fanb: the
 // fan region's bytes (0: beam records instead).
 __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int rowbytes, size_t fanb = 0) {
-  // fold, oold, fp tiles; the square sensor (nbeams == 0) also neg, pos, op
+  // fold, oold, fp tiles; the square sensor (nbeams == 0) also neg, pos, op;
+  // the fan's column planes neg / marks / seen overlay this region
+  const size_t rowplanes = (((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15;
   size_t b = (size_t)(nbeams > 0 ? 3 : 6) * N * TW * TW * 8;
-  b += (((size_t)3 * row_plane_words(N, TW, rowbytes) * rowbytes) + 15) & ~(size_t)15;  // neg / marks / seen rows
+  if (fanb && b < rowplanes) b = rowplanes;
+  b += rowplanes;  // neg / marks / seen rows
   b += fanb ? ((fanb + 15) & ~(size_t)15) : (size_t)(nbeams > 0 ? nbeams : 1) * 16;  // fan region / beams
   b += (((size_t)N * 8 * 4) + 15) & ~(size_t)15;       // x0, y0, x, y, bx, by, dist M / witness
   b += 64;                                             // scalars
@@ -194,7 +197,7 @@ __host__ __device__ inline size_t env_lds_bytes(int N, int TW, int nbeams, int r
 __host__ __device__ inline size_t state_lds_bytes(const State& s, int rowbytes) {
   const bool fan = s.sensor == 0 && s.fan_nsec + s.fan_nspec > 0;
   return env_lds_bytes(s.N, s.TW, s.sensor == 0 ? s.nbeams : 0, rowbytes,
-                       fan ? fan_lds_bytes(s.N, s.TW, rowbytes, s.fan_nspec, s.fan_kt, s.fan_words) : 0);
+                       fan ? fan_lds_bytes(s.N, s.fan_nspec, s.fan_kt, s.fan_words) : 0);
 }
 
 // Byte stride between the env slots of a workgroup: skewed by 20 LDS banks so
