@@ -239,6 +239,10 @@ __device__ __forceinline__ void specialize(State& s) {
     s.nbeams = SH::NB;
     s.mg_nb = magic_div(SH::NB);
   }
+  if constexpr (SH::NB > 0 && SH::NB < 64) {  // sparse beams: never the fan march (build_fan)
+    s.fan_nsec = 0;
+    s.fan_nspec = 0;
+  }
   if constexpr (SH::EGO > 0) {
     s.ego = SH::EGO;
     s.E = 2 * SH::EGO + 1;
