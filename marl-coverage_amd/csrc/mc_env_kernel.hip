@@ -1581,15 +1581,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   // beam records, up to 3 * LPE int4 in this round trip
   const bool fan = fan_on(s);
   const int n16 = fan ? s.fan_words / 4 : 0;
-  const int4* fsrc = reinterpret_cast<const int4*>(s.fan_data);
-  int4 fv[3];
-  if (fan) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int j = C.sub + i * LPE;
-      fv[i] = fsrc[j < n16 ? j : 0];
-    }
-  }
+  const int4* fsrc = reinterpret_cast<const int4*>(fan ? (const void*)s.fan_data : (const void*)s.pos);
+  const int4 fv0 = fsrc[C.sub < n16 ? C.sub : 0];
+  const int4 fv1 = fsrc[C.sub + LPE < n16 ? C.sub + LPE : 0];
+  const int4 fv2 = fsrc[C.sub + 2 * LPE < n16 ? C.sub + 2 * LPE : 0];
   zero_marks<NT, EPW, WT>(s, C);  // overlaps the round trip
   // every result is needed below: keep the compiler from sinking a load into
   // the branch that uses it (that would make it a round trip of its own)
@@ -1624,9 +1619,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   }
   if (fan) {
     int4* dst = reinterpret_cast<int4*>(L.fan);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      if (C.sub + i * LPE < n16) dst[C.sub + i * LPE] = fv[i];
+    if (C.sub < n16) dst[C.sub] = fv0;
+    if (C.sub + LPE < n16) dst[C.sub + LPE] = fv1;
+    if (C.sub + 2 * LPE < n16) dst[C.sub + 2 * LPE] = fv2;
     for (int j = C.sub + 3 * LPE; j < n16; j += LPE) dst[j] = fsrc[j];
   } else if (lidar) {
     if (C.sub < s.nbeams) reinterpret_cast<int4*>(L.beams)[C.sub] = bm0;
