@@ -544,6 +544,29 @@ __global__ __launch_bounds__(256) void sg_step_kernel(SState s, const uint8_t* _
 // masks, and every lane of the robot runs the robot's whole fold from them.
 // Same results as sg_step_kernel<R, GPW> (which takes one lane per robot).
 // --------------------------------------------------------------------------
+// DPP broadcasts inside a 16-lane row (one env of a GPW = 4 wave): lane L of
+// the row (row_share), lane j of each quad (quad_perm), and a row sum into
+// its lane 0 (row_shl steps; lanes shifted in from outside the row read 0)
+template <int L>
+__device__ __forceinline__ int row_share(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x150 | L, 0xF, 0xF, false); }
+template <int L>
+__device__ __forceinline__ double row_share_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)row_share<L>((int)(uint32_t)b), hi = (uint32_t)row_share<L>((int)(uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+template <int J>
+__device__ __forceinline__ int quad_share(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, J | (J << 2) | (J << 4) | (J << 6), 0xF, 0xF, false);
+}
+__device__ __forceinline__ int row_sum_to_lane0(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x101, 0xF, 0xF, true);  // row_shl:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x102, 0xF, 0xF, true);  // row_shl:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0xF, true);  // row_shl:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x108, 0xF, 0xF, true);  // row_shl:8
+  return v;
+}
+
 template <int R, int GPW>
 __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __restrict__ actions,
                                                     const int32_t* __restrict__ quot,
@@ -567,6 +590,9 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
   const int RL = 1 << lgRL;
   const int i = li >> lgRL, q = li & (RL - 1);
   const bool me = valid && i < N;
+  // one env per 16-lane row and one robot per quad, robots in slot order:
+  // broadcasts by DPP instead of LDS shuffles
+  const bool dpp = NG == 16 && RL == 4 && !s.scan;
   auto gballot = [&](bool p) -> uint64_t {
     const uint64_t m = __ballot(p);
     return GPW == 1 ? m : (m >> gb) & low_mask(NG);
@@ -613,7 +639,8 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
       for (int j = 0; j < N; ++j) rank += gshfl(sc, rlane(j)) < sc;
       slot = rank;
     }
-    const int slot_act = gshfl(my_act, rlane(slot < N ? slot : 0));
+    // (without scanning slot = i: every lane of robot i holds its byte)
+    const int slot_act = s.scan ? gshfl(my_act, rlane(slot < N ? slot : 0)) : my_act;
     const int u = me ? slot_act : 255;
     int tx = x, ty = y;
     if (u == 0) tx = x - 1;
@@ -657,12 +684,7 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
     const double dv = (s.dist && inb && u < 4) ? (double)dvr : 0.0;
     // ---- moves in slot order (:121-174), replayed by every lane of a robot ----
     double v = 0.0;
-    for (int k = 0; k < N; ++k) {  // robot z = the one with slot k
-      const int z = s.scan ? ((__ffsll((unsigned long long)gballot(me && q == 0 && slot == k)) - 1) >> lgRL) : k;
-      const int zl = rlane(z);
-      const int zu = gshfl(u, zl);
-      const int zx = gshfl(tx, zl), zy = gshfl(ty, zl);
-      const int zok = gshfl((int)gfree, zl);
+    auto move = [&](int z, int zu, int zx, int zy, int zok) {
       const bool occ = gballot(me && x == zx && y == zy) != 0ull;
       if (zu < 4 && i == z) {  // not a move: nothing happens (no penalty)
         if (zok && !occ) {
@@ -673,12 +695,36 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
           v = v - s.pen;
         }
       }
+    };
+    if constexpr (NG == 16) {
+      if (dpp) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k < N) {
+            const int zl = 4 * k;
+            switch (k) {
+              case 0: move(0, row_share<0>(u), row_share<0>(tx), row_share<0>(ty), row_share<0>((int)gfree)); break;
+              case 1: move(1, row_share<4>(u), row_share<4>(tx), row_share<4>(ty), row_share<4>((int)gfree)); break;
+              case 2: move(2, row_share<8>(u), row_share<8>(tx), row_share<8>(ty), row_share<8>((int)gfree)); break;
+              default: move(3, row_share<12>(u), row_share<12>(tx), row_share<12>(ty), row_share<12>((int)gfree)); break;
+            }
+            (void)zl;
+          }
+        }
+      }
     }
-    if (me && q == 0) {
-      s_x[slot_env][i] = x;
-      s_y[slot_env][i] = y;
+    if (!dpp) {
+      for (int k = 0; k < N; ++k) {  // robot z = the one with slot k
+        const int z = s.scan ? ((__ffsll((unsigned long long)gballot(me && q == 0 && slot == k)) - 1) >> lgRL) : k;
+        const int zl = rlane(z);
+        move(z, gshfl(u, zl), gshfl(tx, zl), gshfl(ty, zl), gshfl((int)gfree, zl));
+      }
+      if (me && q == 0) {
+        s_x[slot_env][i] = x;
+        s_y[slot_env][i] = y;
+      }
+      wave_sync();
     }
-    wave_sync();
     // ---- sense (:177-201): the lane's rows; a cell with grid >= 0 is new
     // unless covered before this step or inside a lower robot's window ----
     const int c0 = y - R;
@@ -699,7 +745,14 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
 #pragma unroll
     for (int m = 0; m < NMAX; ++m) {
       const bool lo = m < N && m < i;
-      const int xm = s_x[slot_env][m < N ? m : 0], ym = s_y[slot_env][m < N ? m : 0];
+      int xm, ym;
+      if (NG == 16 && dpp) {  // robot m's post-move cell from its quad
+        xm = m == 0 ? row_share<0>(x) : (m == 1 ? row_share<4>(x) : (m == 2 ? row_share<8>(x) : row_share<12>(x)));
+        ym = m == 0 ? row_share<0>(y) : (m == 1 ? row_share<4>(y) : (m == 2 ? row_share<8>(y) : row_share<12>(y)));
+      } else {
+        xm = s_x[slot_env][m < N ? m : 0];
+        ym = s_y[slot_env][m < N ? m : 0];
+      }
       lcm[m] = lo ? mask32(max(0, ym - R - c0), min(n, ym + R + 1 - c0)) : 0u;
       lxm[m] = xm;
     }
@@ -735,9 +788,20 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
     const double mfp = -s.fpen;
 #pragma unroll
     for (int jj = 0; jj < n; ++jj) {
-      const int src = gb + rlane(i < N ? i : 0) + (jj & (RL - 1));
-      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)pub64, src);
-      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(pub64 >> 32), src);
+      uint32_t lo, hi;
+      if (NG == 16 && dpp) {  // row lane jj & 3 of this robot's quad
+        const int pl = (int)(uint32_t)pub64, ph = (int)(uint32_t)(pub64 >> 32);
+        switch (jj & 3) {
+          case 0: lo = (uint32_t)quad_share<0>(pl); hi = (uint32_t)quad_share<0>(ph); break;
+          case 1: lo = (uint32_t)quad_share<1>(pl); hi = (uint32_t)quad_share<1>(ph); break;
+          case 2: lo = (uint32_t)quad_share<2>(pl); hi = (uint32_t)quad_share<2>(ph); break;
+          default: lo = (uint32_t)quad_share<3>(pl); hi = (uint32_t)quad_share<3>(ph); break;
+        }
+      } else {
+        const int src = gb + rlane(i < N ? i : 0) + (jj & (RL - 1));
+        lo = (uint32_t)__shfl((int)(uint32_t)pub64, src);
+        hi = (uint32_t)__shfl((int)(uint32_t)(pub64 >> 32), src);
+      }
       const uint64_t w = (uint64_t)lo | ((uint64_t)hi << 32);
       const uint32_t row = (uint32_t)(w >> (24 * (jj >> lgRL)));
       const uint32_t nw = row & 0xFFu, ge0 = (row >> 8) & 0xFFu, fpos = (row >> 16) & 0xFFu;
@@ -788,15 +852,29 @@ __global__ __launch_bounds__(256) void sg_step_rows(SState s, const uint8_t* __r
     if ((qt < 0 || qt >= 4) && valid && li == 0) atomicOr(s.err, ERR_KEY);
     v = v + ((qt == ap) ? 0.0 : -1.0);
     if (lead) {
-      s_v[slot_env][slot] = v;
+      if (!dpp) s_v[slot_env][slot] = v;
       s.pos[((size_t)e * N + i) * 2] = x;
       s.pos[((size_t)e * N + i) * 2 + 1] = y;
     }
+    double total = 0.0;
+    if (NG == 16 && dpp) {
+      cnt = row_sum_to_lane0(cnt);  // group sum in lane 0
+      // the slots' rewards from their quads, summed as np.sum does below 8
+      // values: sequentially from -0.0 (np_pairwise_sum)
+      const double v0 = row_share_f64<0>(v), v1 = row_share_f64<4>(v);
+      const double v2 = row_share_f64<8>(v), v3 = row_share_f64<12>(v);
+      total = -0.0;
+      total += v0;
+      if (N > 1) total += v1;
+      if (N > 2) total += v2;
+      if (N > 3) total += v3;
+    } else {
 #pragma unroll
-    for (int o = NG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);  // group sum
-    wave_sync();
+      for (int o = NG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);  // group sum
+      wave_sync();
+      if (valid && li == 0) total = np_pairwise_sum(s_v[slot_env], N);
+    }
     if (valid && li == 0) {
-      double total = np_pairwise_sum(s_v[slot_env], N);
       const int cs = cs0 + 1;
       const uint32_t cc = cc0 + (uint32_t)cnt;
       const double pc = (double)cc / (double)npos;
