@@ -49,24 +49,61 @@ namespace mc {
 namespace {
 constexpr int kDtThreads = 512;
 constexpr int kStrip = 32;                     // columns per strip
-constexpr int kChunks = kDtThreads / kStrip;   // row chunks per column in the column pass
-// LDS strides, padded off the bank period: a strip row is 36 u16 (72 B = 18
+constexpr int kPairs = kStrip / 2;             // column pairs (packed u16 halves) per strip
+constexpr int kCh = kDtThreads / kPairs;       // row chunks per column pair: the 32 lanes of a half wave
+// LDS stride, padded off the bank period: a strip row is 36 u16 (72 B = 18
 // dwords: the row pass's 8-byte stores of 16 consecutive rows hit 32
-// distinct banks; at 64 B four rows shared each bank), a column's chunk
-// minima 20 u32 (the column pass's 16-byte reads of 16 columns hit distinct
-// banks; at 16 u32 four columns shared them)
+// distinct banks; at 64 B four rows shared each bank; the column pass's
+// dword reads of 32 chunks 17 rows apart hit 32 distinct banks)
 constexpr int kSP = 36;
-constexpr int kCM = 20;
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
-constexpr int kRowOff = 1024;                  // min(g - u) + kRowOff >= 0 (u < kMaxRows)
+constexpr int kRowOff = 1024;                  // g - u + kRowOff > 0 (u < kMaxRows)
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+constexpr u16x2 kNone2 = {0xFFFF, 0xFFFF};
+constexpr u16x2 kRowOff2 = {kRowOff, kRowOff};
+__device__ __forceinline__ u16x2 splat2(int v) { return u16x2{(uint16_t)v, (uint16_t)v}; }
+
+// Packed minima across the 32 chunks of a column pair (lane c of a half wave
+// = chunk c): over the chunks before this one / after it (0xFFFF: none).
+// DPP row shifts inside each 16-lane row, the other row's total by readlane.
+template <int CTRL>
+__device__ __forceinline__ u16x2 dpp2(u16x2 v) {  // source lane out of the row: 0xFFFF pair
+  return __builtin_bit_cast(u16x2, __builtin_amdgcn_update_dpp((int)0xFFFFFFFF, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ u16x2 excl_prefix_min32(u16x2 v) {
+  const int l = threadIdx.x & 63;
+  u16x2 x = __builtin_elementwise_min(v, dpp2<0x111>(v));  // row_shr:1
+  x = __builtin_elementwise_min(x, dpp2<0x112>(x));        // row_shr:2
+  x = __builtin_elementwise_min(x, dpp2<0x114>(x));        // row_shr:4
+  x = __builtin_elementwise_min(x, dpp2<0x118>(x));        // row_shr:8: inclusive within the row
+  const u16x2 r0 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  const u16x2 r2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 47));
+  const u16x2 carry = (l & 16) ? ((l & 32) ? r2 : r0) : kNone2;  // rows 1, 3: the row before
+  u16x2 e = dpp2<0x111>(x);                                     // exclusive within the row
+  e = (l & 15) == 0 ? kNone2 : e;
+  return __builtin_elementwise_min(e, carry);
+}
+__device__ __forceinline__ u16x2 excl_suffix_min32(u16x2 v) {
+  const int l = threadIdx.x & 63;
+  u16x2 x = __builtin_elementwise_min(v, dpp2<0x101>(v));  // row_shl:1
+  x = __builtin_elementwise_min(x, dpp2<0x102>(x));        // row_shl:2
+  x = __builtin_elementwise_min(x, dpp2<0x104>(x));        // row_shl:4
+  x = __builtin_elementwise_min(x, dpp2<0x108>(x));        // row_shl:8
+  const u16x2 r1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 16));
+  const u16x2 r3 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 48));
+  const u16x2 carry = (l & 16) ? kNone2 : ((l & 32) ? r3 : r1);  // rows 0, 2: the row after
+  u16x2 e = dpp2<0x101>(x);
+  e = (l & 15) == 15 ? kNone2 : e;
+  return __builtin_elementwise_min(e, carry);
+}
 }  // namespace
 
-// rows per column chunk: the instantiation (16, 33 or 52) whose kChunks
-// chunks cover RX; the strip holds kChunks * chunk rows (rows >= RX are
-// padding with no covered cell)
-__host__ __device__ constexpr int chunk_rows(int RX) { return RX <= 256 ? 16 : (RX <= 528 ? 33 : 52); }
+// rows per column chunk: the instantiation (8, 17 or 26) whose kCh chunks
+// cover RX; the strip holds kCh * chunk rows (rows >= RX are padding with
+// no covered cell)
+__host__ __device__ constexpr int chunk_rows(int RX) { return RX <= 256 ? 8 : (RX <= 544 ? 17 : 26); }
 
 // LDS carve of the full transform (bytes): row bitboard | strip (u16, also the
 // tile staging area) | chunk minima | targets
@@ -77,9 +114,9 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   DtLds L;
   const int RW = (RY + 63) >> 6;
   L.cb = (size_t)RX * RW * 8;
-  const size_t st = (size_t)kChunks * chunk_rows(RX) * kSP * 2, tiles = (size_t)MT * 8;
+  const size_t st = (size_t)kCh * chunk_rows(RX) * kSP * 2, tiles = (size_t)MT * 8;
   L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
-  L.mins = (size_t)2 * kStrip * kCM * 4;
+  L.mins = 0;
   L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
   L.total = L.cb + L.strip + L.mins + L.tgt;
   return L;
@@ -100,9 +137,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   const int T = post ? 5 + E * E : 5;
   const DtLds LL = dt_lds(RX, RY, s.MT, 5 + E * E);
   uint64_t* Cb = reinterpret_cast<uint64_t*>(smem);
-  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kChunks * kCL][kSP] (kStrip used)
-  constexpr int RXP = kChunks * kCL;                         // strip rows incl. padding
-  uint32_t* s_cmin = reinterpret_cast<uint32_t*>(smem + LL.cb + LL.strip);  // [2][kStrip][kCM] (kChunks used)
+  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.cb);  // [kCh * kCL][kSP] (kStrip used)
+  constexpr int RXP = kCh * kCL;                             // strip rows incl. padding
   int* s_d = reinterpret_cast<int*>(smem + LL.cb + LL.strip + LL.mins);
   const uint64_t last = (RY & 63) ? low_mask(RY & 63) : ~0ull;
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
@@ -155,9 +191,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // row-pass registers: a thread owns rows tid and tid + kDtThreads
     int lastL[2] = {-kInf, -kInf};  // last covered column left of the strip
     int nrw[2] = {-1, -1};          // next non-empty word after the current one (-1: not scanned)
-    const int col = tid % kStrip, chunk = tid / kStrip;
+    const int chunk = tid & (kCh - 1), pair = tid / kCh;
     const int u0c = chunk * kCL;
-    // best (d << 16 | u) of this thread and its column (ties: the largest u)
+    // the chunk's rows inside the grid (only the last chunk has padding)
+    const int nin = max(min(RX - u0c, kCL), 0);
+    const uint32_t rowmask = nin >= 32 ? ~0u : ((1u << nin) - 1u);
+    // best (d << 16 | u) of this thread's cells (ties: the largest u)
     uint32_t bestkey = 0;
     int bestv = -1;
     // bounding box of the target cells (extended coordinates): the column
@@ -232,82 +271,68 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         for (int k = 0; k < 8; ++k) grow[k] = make_uint2(pk[2 * k], pk[2 * k + 1]);
       }
       __syncthreads();
-      // ---- column pass: this thread's chunk of column c0 + col into registers.
-      // u0 is made opaque per strip: the compiler would otherwise hoist kCL
-      // loop-invariant row values out of the strip loop (and spill them)
+      // ---- column pass: column pair p (columns c0 + 2p, c0 + 2p + 1 as the
+      // low / high u16 halves of one packed register; saturating u16 pairs,
+      // 0xFFFF = no covered cell) over chunk c of kCL rows.  u0 is made opaque
+      // per strip: the compiler would otherwise hoist kCL loop-invariant row
+      // values out of the strip loop (and spill them)
       int u0 = u0c;
       asm volatile("" : "+v"(u0));
-      int gv[kCL];
-      int pmin = kInf, smin = kInf;
-      uint16_t* gcol = G + u0 * kSP + col;  // row u0 + i at gcol[i * kSP]
+      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(G) + u0 * (kSP / 2) + pair;
+      u16x2 tp[kCL], sd[kCL];  // g + K - u (then d), g + u (then the "down" distance)
+      u16x2 pm = kNone2, sm = kNone2;
 #pragma unroll
       for (int i = 0; i < kCL; ++i) {
-        gv[i] = (int)gcol[i * kSP];
-        pmin = min(pmin, gv[i] - (u0 + i));
-        smin = min(smin, gv[i] + (u0 + i));
+        const u16x2 g = __builtin_bit_cast(u16x2, g32[i * (kSP / 2)]);
+        const u16x2 uu = splat2(u0 + i);
+        tp[i] = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(g, kRowOff2), uu);
+        sd[i] = __builtin_elementwise_add_sat(g, uu);
+        pm = __builtin_elementwise_min(pm, tp[i]);
+        sm = __builtin_elementwise_min(sm, sd[i]);
       }
-      // chunk minima, packed: low half min(g - u) + RXOFF, high half min(g + u)
-      uint32_t* cmin = s_cmin + (st & 1) * (kStrip * kCM);  // double buffer: 2 barriers per strip
-      cmin[col * kCM + chunk] =
-          (uint32_t)min(pmin + kRowOff, 0xFFFF) | ((uint32_t)min(smin, 0xFFFF) << 16);
-      __syncthreads();
-      u16x2 accP = {0xFFFF, 0xFFFF}, accS = {0xFFFF, 0xFFFF};
-      {
-        const uint4* cm = reinterpret_cast<const uint4*>(cmin + col * kCM);
-#pragma unroll
-        for (int k = 0; k < kChunks / 4; ++k) {
-          const uint4 q4 = cm[k];
-          const uint32_t qv[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-          for (int l = 0; l < 4; ++l) {
-            const int q = 4 * k + l;
-            const u16x2 val = __builtin_bit_cast(u16x2, qv[l]);
-            const u16x2 none = {0xFFFF, 0xFFFF};
-            accP = __builtin_elementwise_min(accP, q < chunk ? val : none);
-            accS = __builtin_elementwise_min(accS, q > chunk ? val : none);
-          }
-        }
-      }
-      // minima over the chunks before / after this one
-      int run = (int)accP.x - kRowOff, sfx = (int)accS.y;
-      if (accP.x == 0xFFFF) run = kInf;
-      if (accS.y == 0xFFFF) sfx = kInf;
+      __syncthreads();  // every G read of the strip is done: the next row pass may write
+      // minima over the pair's chunks before / after this one (its 32 chunks
+      // are the lanes of one half wave)
+      u16x2 run = excl_prefix_min32(pm), sfx = excl_suffix_min32(sm);
       // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u
-      // (u16 pairs: register budget of two workgroups per CU)
-      uint32_t dnp[(kCL + 1) / 2];
 #pragma unroll
       for (int i = kCL - 1; i >= 0; --i) {
-        sfx = min(sfx, gv[i] + (u0 + i));
-        const uint32_t dn = (uint32_t)min(sfx - (u0 + i), 0xFFFF);
-        if (i & 1) dnp[i >> 1] = dn << 16;
-        else dnp[i >> 1] = (i + 1 < kCL ? dnp[i >> 1] : 0u) | dn;
+        sfx = __builtin_elementwise_min(sfx, sd[i]);
+        sd[i] = __builtin_elementwise_sub_sat(sfx, splat2(u0 + i));
       }
-      const int v = c0 + col;
-      const bool keep = v >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
-      uint32_t key = 0;
-      // rows of this chunk inside the grid (only the last chunk has padding)
-      const int nin = max(RX - u0, 0);
-      const uint64_t vm = nin >= kCL ? ~0ull : ((1ull << nin) - 1ull);
+      // prefix scan, d = min(up, down), the best (d << 16 | u) of each column
+      // over the chunk's grid rows (the last chunk's padding rows count 0)
+      uint32_t klo = 0, khi = 0;
 #pragma unroll
       for (int i = 0; i < kCL; ++i) {
-        run = min(run, gv[i] - (u0 + i));
-        gv[i] = min(u0 + i + run, (int)((dnp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu));  // d
-        const uint32_t k = ((uint32_t)gv[i] << 16) | (uint32_t)(u0 + i);
-        key = max(key, ((vm >> i) & 1ull) ? k : 0u);
+        const u16x2 uu = splat2(u0 + i);
+        run = __builtin_elementwise_min(run, tp[i]);
+        const u16x2 up = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(run, uu), kRowOff2);
+        const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(up, sd[i])) &
+                           (uint32_t)__builtin_amdgcn_sbfe((int)rowmask, i, 1);
+        tp[i] = __builtin_bit_cast(u16x2, d);
+        klo = max(klo, (d << 16) | (uint32_t)(u0 + i));
+        khi = max(khi, (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
       }
-      if (v < RY && key > bestkey) {
-        bestkey = key;
+      const int v = c0 + 2 * pair;
+      if (v < RY && klo > bestkey) {
+        bestkey = klo;
         bestv = v;
       }
-      if (keep) {  // the target cells of this column chunk, from registers
+      if (v + 1 < RY && khi > bestkey) {
+        bestkey = khi;
+        bestv = v + 1;
+      }
+      const bool keep = v + 1 >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
+      if (keep) {  // the target cells of this chunk's columns, from registers
         for (int t = 0; t < T; ++t) {
           int tu, tv;
           target(t, tu, tv);
-          if (tv == v && tu >= u0 && tu < u0 + kCL && tu < RX) {
-            int val = 0;
+          if ((tv == v || tv == v + 1) && tu >= u0 && tu < u0 + kCL && tu < RX) {
+            uint32_t val = 0;
 #pragma unroll
-            for (int i = 0; i < kCL; ++i) val = (u0 + i == tu) ? gv[i] : val;
-            s_d[t] = min(val, 0xFFFF);
+            for (int i = 0; i < kCL; ++i) val = (u0 + i == tu) ? __builtin_bit_cast(uint32_t, tp[i]) : val;
+            s_d[t] = (int)(tv == v ? (val & 0xFFFFu) : (val >> 16));
           }
         }
       }
@@ -382,9 +407,9 @@ static hipError_t launch_full(const State& s, int pad, int post, float* pre_out,
     hipLaunchKernelGGL(dist_kernel_t<CL>, dim3(grid), dim3(kDtThreads), lds, stream, s, pad,   \
                        post, pre_out, dist_obs, list, count);                                  \
   } while (0)
-  if (cl == 16) MC_DT(16);
-  else if (cl == 33) MC_DT(33);
-  else MC_DT(52);  // kMaxRows / kChunks
+  if (cl == 8) MC_DT(8);
+  else if (cl == 17) MC_DT(17);
+  else MC_DT(26);  // kMaxRows / kCh
 #undef MC_DT
   return hipGetLastError();
 }

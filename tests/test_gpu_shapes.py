@@ -136,7 +136,7 @@ def test_c5_shape_512_per_step(torch_cuda):
     envs through the C5 instantiation: 8 envs compared with the oracle every
     step from the reset for 30 steps, and every known (max d, witness) of those
     envs checked against a fresh transform every step.  RX = 518 extended rows
-    runs the full transform as dist_kernel_t<33> (mc_dist.hip chunk_rows)."""
+    runs the full transform as dist_kernel_t<17> (mc_dist.hip chunk_rows)."""
     import marlcov
     from marlcov import _lib
     torch = torch_cuda
@@ -153,21 +153,24 @@ def test_c5_shape_512_per_step(torch_cuda):
     run_against_oracle(torch, env, cfg, rs, 30, sample, 5, "c5_512", dist_check=True, sentinel_p=0.0)
 
 
-def test_dist_kernel_52_rows(torch_cuda):
-    """Extended maps of 529..832 rows run the transform as dist_kernel_t<52>:
-    a 600 x 40 grid (RX = 606) with dist_reward, per step against the oracle."""
+@pytest.mark.parametrize("rows,rx", [(600, 606), (538, 544)], ids=["rx606_kcl26", "rx544_kcl17_full"])
+def test_dist_kernel_long_maps(torch_cuda, rows, rx):
+    """Extended maps of 545..832 rows run the transform as dist_kernel_t<26>
+    (a 600 x 40 grid, RX = 606); RX = 544 fills the 32 chunks of 17 rows of
+    dist_kernel_t<17> exactly (no padding row).  dist_reward, per step
+    against the oracle."""
     import marlcov
     from marlcov import _lib
     torch = torch_cuda
     cfg = base_cfg(numrobot=2, dist_reward=1, sensor_config={"num_lasers": 9, "range": 4})
-    rs = np.random.RandomState(52)
+    rs = np.random.RandomState(rows)
     B = 4
-    grids = [bern(rs, 600, 40, 0.1) for _ in range(B)]
+    grids = [bern(rs, rows, 40, 0.1) for _ in range(B)]
     env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False)
-    assert 529 <= env.width + 2 * env.pad <= 832
+    assert env.width + 2 * env.pad == rx
     env.reset()
     assert int(env.get_state(_lib.FIELD_DIST_LISTED).item()) > 0
-    run_against_oracle(torch, env, cfg, rs, 20, list(range(B)), 0, "dist52", dist_check=True, sentinel_p=0.0)
+    run_against_oracle(torch, env, cfg, rs, 20, list(range(B)), 0, f"dist{rx}", dist_check=True, sentinel_p=0.0)
 
 
 # ---------------------------------------------------------------------------
