@@ -114,7 +114,9 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   DtLds L;
   const int RW = (RY + 63) >> 6;
   L.cb = (size_t)RX * RW * 8;
-  const size_t st = (size_t)kCh * chunk_rows(RX) * kSP * 2, tiles = (size_t)MT * 8;
+  // the strip area also holds the map's rows while the row bitboard is built
+  // (at most RX x RW words)
+  const size_t st = (size_t)kCh * chunk_rows(RX) * kSP * 2, tiles = (size_t)RX * RW * 8;
   L.strip = ((st > tiles ? st : tiles) + 15) & ~(size_t)15;
   L.mins = 0;
   L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
@@ -170,16 +172,40 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       s_cov = 0;
     }
     {
-      // the agent's tiles into LDS first (coalesced, all loads in flight; the
-      // strip area is free until the strips start), then the row bitboard
-      uint64_t* tl = reinterpret_cast<uint64_t*>(G);
+      // the agent's tiles (coalesced loads) scattered as row bytes into map
+      // rows in the strip area (free until the strips start): byte tj of map
+      // row X = row X & 7 of tile (X >> 3, tj); the bytes past the last tile
+      // column are zeroed by their row's thread.  Then the extended rows:
+      // map columns shifted right by pad (a funnel shift of two words)
+      uint8_t* crow = reinterpret_cast<uint8_t*>(G);
+      const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
+      const int RB = RWm * 8;           // bytes per map row
 #pragma unroll 4
-      for (int i = tid; i < s.MT; i += kDtThreads) tl[i] = free_t[i];
+      for (int i = tid; i < s.MT; i += kDtThreads) {
+        const uint64_t t = free_t[i];
+        const int blk = i >> 4, bi = blk / s.TCS, bj = blk - bi * s.TCS;
+        const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
+        if (ti < s.TR && tj < s.TC) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(t >> (8 * r));
+        }
+      }
+      for (int X = tid; X < s.Wp; X += kDtThreads)
+        for (int b = s.TC; b < RB; ++b) crow[(size_t)X * RB + b] = 0;
       __syncthreads();
+      const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
       int any = 0;
       for (int i = tid; i < RX * RW; i += kDtThreads) {
-        const int u = i / RW, w = i - u * RW;
-        const uint64_t c = row_word(s, tl, pad, u, w) & ((w == RW - 1) ? last : ~0ull);
+        const int u = i / RW, w = i - u * RW, X = u - pad;
+        uint64_t c = 0;
+        if (X >= 0 && X < s.Wp) {  // map columns [64 w - pad, 64 w - pad + 64)
+          const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
+          const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
+          const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
+          c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
+        }
+        c &= (w == RW - 1) ? last : ~0ull;
         Cb[i] = c;
         any |= c != 0;
       }
