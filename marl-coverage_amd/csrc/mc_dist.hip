@@ -320,53 +320,33 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       // minima over the pair's chunks before / after this one (its 32 chunks
       // are the lanes of one half wave)
       u16x2 run = excl_prefix_min32(pm), sfx = excl_suffix_min32(sm);
-      // suffix and prefix scans, each as two half-chunk chains (independent,
-      // so they interleave) joined afterwards: the "down" distance
-      // min_{u'>=u} g(u') + u' - u and the "up" distance u + min_{u'<=u} g(u') - u'
-      constexpr int H = kCL / 2;
-      u16x2 sa = sfx, sb = kNone2, ra = run, rb = kNone2;
+      // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u
 #pragma unroll
-      for (int k = 0; k < kCL - H; ++k) {
-        sa = __builtin_elementwise_min(sa, sd[kCL - 1 - k]);
-        sd[kCL - 1 - k] = sa;
-        if (k < H) {
-          sb = __builtin_elementwise_min(sb, sd[H - 1 - k]);
-          sd[H - 1 - k] = sb;
-        }
+      for (int i = kCL - 1; i >= 0; --i) {
+        sfx = __builtin_elementwise_min(sfx, sd[i]);
+        sd[i] = __builtin_elementwise_sub_sat(sfx, splat2(u0 + i));
       }
-#pragma unroll
-      for (int k = 0; k < kCL - H; ++k) {
-        if (k < H) {
-          ra = __builtin_elementwise_min(ra, tp[k]);
-          tp[k] = ra;
-        }
-        rb = __builtin_elementwise_min(rb, tp[H + k]);
-        tp[H + k] = rb;
-      }
-      // d = min(up, down), the best (d << 16 | u) of each column over the
-      // chunk's grid rows (the last chunk's padding rows count 0)
-      uint32_t klo[2] = {0, 0}, khi[2] = {0, 0};
+      // prefix scan, d = min(up, down), the best (d << 16 | u) of each column
+      // over the chunk's grid rows (the last chunk's padding rows count 0)
+      uint32_t klo = 0, khi = 0;
 #pragma unroll
       for (int i = 0; i < kCL; ++i) {
         const u16x2 uu = splat2(u0 + i);
-        const u16x2 pre = i < H ? tp[i] : __builtin_elementwise_min(tp[i], ra);
-        const u16x2 suf = i < H ? __builtin_elementwise_min(sd[i], sa) : sd[i];
-        const u16x2 up = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(pre, uu), kRowOff2);
-        const u16x2 dn = __builtin_elementwise_sub_sat(suf, uu);
-        const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(up, dn)) &
+        run = __builtin_elementwise_min(run, tp[i]);
+        const u16x2 up = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(run, uu), kRowOff2);
+        const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(up, sd[i])) &
                            (uint32_t)__builtin_amdgcn_sbfe((int)rowmask, i, 1);
         tp[i] = __builtin_bit_cast(u16x2, d);
-        klo[i & 1] = max(klo[i & 1], (d << 16) | (uint32_t)(u0 + i));
-        khi[i & 1] = max(khi[i & 1], (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
+        klo = max(klo, (d << 16) | (uint32_t)(u0 + i));
+        khi = max(khi, (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
       }
-      const uint32_t klo_m = max(klo[0], klo[1]), khi_m = max(khi[0], khi[1]);
       const int v = c0 + 2 * pair;
-      if (v < RY && klo_m > bestkey) {
-        bestkey = klo_m;
+      if (v < RY && klo > bestkey) {
+        bestkey = klo;
         bestv = v;
       }
-      if (v + 1 < RY && khi_m > bestkey) {
-        bestkey = khi_m;
+      if (v + 1 < RY && khi > bestkey) {
+        bestkey = khi;
         bestv = v + 1;
       }
       const bool keep = v + 1 >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
