@@ -476,6 +476,47 @@ def test_fan_exceptional_starts(torch_cuda):
     env.check()
 
 
+# dense beam sets over a spread of beam counts, ranges and window widths
+# (32- and 64-bit rows, sector sizes 1..6, specials or none): the fan march
+# against the oracle
+FAN_SWEEP = [(64, 6.0, 2, 24, 30), (96, 9.5, 3, 30, 26), (200, 12.0, 2, 34, 40), (256, 15.0, 4, 50, 44),
+             (450, 18.0, 3, 60, 60), (720, 22.0, 2, 70, 64), (361, 25.5, 5, 80, 70), (512, 27.0, 1, 90, 90)]
+
+
+@pytest.mark.parametrize("nb,rng,n,w,l", FAN_SWEEP, ids=[f"b{c[0]}_r{c[1]}" for c in FAN_SWEEP])
+def test_fan_sweep(torch_cuda, nb, rng, n, w, l):
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=n, allow_even_beams=True, sensor_config={"num_lasers": nb, "range": rng})
+    rs = np.random.RandomState(nb)
+    B, T = 3, 8
+    grids = [bern(rs, w, l, 0.12) for _ in range(B)]
+    refs, pos = [], []
+    for b in range(B):
+        np.random.seed(500 + b)
+        r = DecGridRLRef([grids[b]], cfg)
+        refs.append(r)
+        pos.append(np.stack([r._xinds, r._yinds], 1))
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False)
+    assert "+fan(" in env.kernel_variant(), env.kernel_variant()
+    env.reset(positions=np.stack(pos))
+    st = device_state(env)
+    for b in range(B):
+        compare_env(st, b, refs[b], f"b{nb} reset env {b}")
+    for t in range(T):
+        acts = rs.randint(0, 4, size=(B, n)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h = full_obs(env, obs, cfg), rew.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"b{nb} t={t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+    env.check()
+
+
 @pytest.mark.parametrize("name", FAN_CASES)
 def test_batch_matches_oracle_ray_march(torch_cuda, name, monkeypatch):
     """The dense cases with the ray march (MARLCOV_FAN=0) instead of the
