@@ -502,13 +502,8 @@ static bool build_fan(const std::vector<mc::Beam>& bt, const std::vector<uint64_
         if ((A >> i) & 1) lit |= 1 << r[i];      // spread: beams A -> their cells
         if ((A >> r[i]) & 1) kill |= 1 << i;     // expand: cells A -> the beams on them
       }
-#ifdef MC_FAN_LUT_T
-      lut[A * 32 + D] = (uint8_t)lit;
-      lut[2048 + A * 32 + D] = (uint8_t)kill;
-#else
       lut[D * 64 + A] = (uint8_t)lit;
       lut[2048 + D * 64 + A] = (uint8_t)kill;
-#endif
     }
   }
   auto cbits = [](const mc::Beam& o) {
@@ -530,11 +525,7 @@ static bool build_fan(const std::vector<mc::Beam>& bt, const std::vector<uint64_
         if (j + 1 < v.size() && off(bt[v[j + 1]], k) != off(bt[v[j]], k)) D |= 1u << j;
         if (bt[v[j]].K >= k) valid |= 1u << j;
       }
-#ifdef MC_FAN_LUT_T
-      out.push_back(D | ((uint32_t)(lo + 32) << 5) | (valid << 16));
-#else
       out.push_back((uint32_t)(lo + 32) | (D << 6) | (valid << 16));
-#endif
     }
   }
   for (int b : spec) {

@@ -835,29 +835,17 @@ __device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, con
       if (KM > 0 ? (k0 + u <= KM) : (k0 + u <= kt)) {
         e[u] = T[k0 + u];
         const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-#ifdef MC_FAN_LUT_T
-        const int sh = bb + (int)((e[u] >> 5) & 63u);
-#else
         const int sh = bb + (int)(e[u] & 63u);
-#endif
         F[u] = (uint32_t)(*lds_ptr<const WT>(P) >> sh) & 63u;
         SN[u] = (uint32_t)(*lds_ptr<const WT>(P + 2 * MD) >> sh) & 63u;
       }
     }
 #pragma unroll
-#ifdef MC_FAN_LUT_T
-    for (int u = 0; u < SU; ++u) kill[u] = expand[(F[u] << 5) | (e[u] & 31u)];
-#else
     for (int u = 0; u < SU; ++u) kill[u] = expand[(e[u] & 0x7C0u) | F[u]];
-#endif
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
       A &= e[u] >> 16;  // in range (a step past the trip count has e = 0)
-#ifdef MC_FAN_LUT_T
-      lit[u] = spread[(A << 5) | (e[u] & 31u)];
-#else
       lit[u] = spread[(e[u] & 0x7C0u) | A];
-#endif
       A &= ~kill[u];
     }
 #pragma unroll
@@ -865,11 +853,7 @@ __device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, con
       const uint32_t nm = lit[u] & ~SN[u];
       if (nm) {
         const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-#ifdef MC_FAN_LUT_T
-        lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)((e[u] >> 5) & 63u)));
-#else
         lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)(e[u] & 63u)));
-#endif
       }
     }
   }
@@ -921,11 +905,7 @@ __device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>
       int lo = 0;
       for (int k = 1; k <= kt; ++k) {
         lo += ((spw >> (k - 1)) & 1u) ? msign : 0;
-#ifdef MC_FAN_LUT_T
-        W[k] = ((uint32_t)(lo + 32) << 5) | (K >= k ? (1u << 16) : 0u);
-#else
         W[k] = (uint32_t)(lo + 32) | (K >= k ? (1u << 16) : 0u);
-#endif
       }
       fan_sector<WT, KM>(s, L, W, a, 1u, kt);
     }
