@@ -400,6 +400,23 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     }
     E->s.dist_mw = (int32_t*)mw;
     E->dist_list = (uint32_t*)lq;
+    // the top-cell cache (mc_dist.hip), off with map sharing (other agents'
+    // maps add cells outside the agent's own sensing windows) or
+    // MARLCOV_DIST_CACHE=0
+    const char* dc = getenv("MARLCOV_DIST_CACHE");
+    if (!c.map_sharing && !(dc && dc[0] == '0')) {
+      void *cc = nullptr, *cd = nullptr, *ch = nullptr;
+      const size_t maps = (size_t)s.B * s.N;
+      if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
+          dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess) {
+        std::string msg = g_err;
+        mc_destroy(E);
+        return fail(MC_EHIP, "dist_reward cache: %s", msg.c_str());
+      }
+      E->s.dist_cc = (int32_t*)cc;
+      E->s.dist_cd = (int32_t*)cd;
+      E->s.dist_ch = (int32_t*)ch;
+    }
   }
   mc_layout& L = E->lay;
   L.tile_rows = 4 * s.TRS;
@@ -890,6 +907,8 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   E->dist_pre_stale = true;  // uploaded maps / positions: recompute the PRE terms
   if (E->s.dist_mw)  // and max(d) of every map
     HIP_TRY(hipMemsetAsync(E->s.dist_mw, 0xFF, (size_t)E->s.B * E->s.N * 8, (hipStream_t)stream));
+  if (E->s.dist_ch)  // and the top-cell caches
+    HIP_TRY(hipMemsetAsync(E->s.dist_ch, 0xFF, (size_t)E->s.B * E->s.N * 32, (hipStream_t)stream));
   return MC_OK;
 }
 

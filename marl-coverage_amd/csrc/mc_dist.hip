@@ -59,6 +59,8 @@ constexpr int kSP = 36;
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
 constexpr int kRowOff = 1024;                  // g - u + kRowOff > 0 (u < kMaxRows)
+constexpr int kMaxTrack = 64;                  // strips whose max(d) the cache pass can skip by
+constexpr int kFastTiles = 2048;               // tiles the cache fast path stages (box + 25 around the robot)
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 constexpr u16x2 kNone2 = {0xFFFF, 0xFFFF};
 constexpr u16x2 kRowOff2 = {kRowOff, kRowOff};
@@ -98,6 +100,34 @@ __device__ __forceinline__ u16x2 excl_suffix_min32(u16x2 v) {
   e = (l & 15) == 15 ? kNone2 : e;
   return __builtin_elementwise_min(e, carry);
 }
+// L1 distance from cell (cx, cy) to the nearest set bit of tile nb (origin
+// (x0, y0)), or cap when none is nearer (the tile-box bound first)
+__device__ __forceinline__ int tile_min_dist(uint64_t nb, int x0, int y0, int cx, int cy, int cap) {
+  const int bx = max(0, max(x0 - cx, cx - (x0 + 7)));
+  const int by = max(0, max(y0 - cy, cy - (y0 + 7)));
+  if (!nb || bx + by >= cap) return cap;
+  const int p = cy - y0;  // the cell's column relative to the tile
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)(nb >> (8 * r)) & 0xFFu;
+    if (!row) continue;
+    int dy;
+    if (p < 0) dy = __ffs(row) - 1 - p;
+    else if (p > 7) dy = p - (31 - __clz(row));
+    else {
+      const uint32_t lo = row & ((2u << p) - 1u), hi = row >> p;
+      dy = lo ? p - (31 - __clz(lo)) : 8;
+      if (hi) dy = min(dy, __ffs(hi) - 1);
+    }
+    cap = min(cap, abs(x0 + r - cx) + dy);
+  }
+  return cap;
+}
+
+// max over the wave (every lane gets it)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
 }  // namespace
 
 // rows per column chunk: the instantiation (8, 17 or 26) whose kCh chunks
@@ -133,6 +163,14 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_cov;
   __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
+  // top-cell cache (State::dist_ch): the fast path's best (d << 16 | index),
+  // the strips' max(d), the cache pass's cell list
+  __shared__ uint32_t s_fkey;
+  __shared__ int s_ffail;
+  __shared__ int s_ccount;
+  __shared__ int s_smax[kMaxTrack];
+  __shared__ int32_t s_ccell[kDistK];
+  __shared__ int s_cdv[kDistK];
   const int tid = threadIdx.x;
   const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6;
   const int E = s.E;
@@ -170,49 +208,134 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     if (tid == 0) {
       s_key = 0;
       s_cov = 0;
+      s_fkey = 0;
+      s_ffail = 0;
+      s_ccount = 0;
     }
-    {
-      // the agent's tiles (coalesced loads) scattered as row bytes into map
-      // rows in the strip area (free until the strips start): byte tj of map
-      // row X = row X & 7 of tile (X >> 3, tj); the bytes past the last tile
-      // column are zeroed by their row's thread.  Then the extended rows:
-      // map columns shifted right by pad (a funnel shift of two words)
-      uint8_t* crow = reinterpret_cast<uint8_t*>(G);
-      const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
-      const int RB = RWm * 8;           // bytes per map row
+    for (int i = tid; i < kMaxTrack; i += kDtThreads) s_smax[i] = 0;
+    // the map's top-cell cache (mc_internal.h State::dist_ch)
+    int ccnt = -1, cM0 = 0, bx0 = 0, by0 = 0, bx1 = -1, by1 = -1;
+    if (s.dist_ch) {
+      const int4 h0 = reinterpret_cast<const int4*>(s.dist_ch + (size_t)ea * 8)[0];
+      const int2 h1 = reinterpret_cast<const int2*>(s.dist_ch + (size_t)ea * 8)[2];
+      ccnt = h0.x;
+      cM0 = h0.y;
+      bx0 = h0.z;
+      by0 = h0.w;
+      bx1 = h1.x;
+      by1 = h1.y;
+    }
+    // ---- fast path for a listed map with a cache: the cells covered since
+    // the cached d were exact all lie in the box, so the current d of a cached
+    // cell is min(its d, the distance to the box's covered cells).  Every
+    // other cell had d < M0 - kDistT when the cache was taken, and d only
+    // decreases: if some cached cell still has d >= M0 - kDistT, the largest
+    // such d is max(d) and that cell a witness.  The targets (all within a
+    // few cells of the robot, whose own cell is covered) come from the tiles
+    // around the robot.
+    bool fast = false;
+    if (list != nullptr && ccnt > 0) {
+      const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
+      const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
+      const int nt = nbr * nbc;
+      const int rti0 = (px >> 3) - 2, rtj0 = (py >> 3) - 2;  // 5 x 5 tiles around the robot
+      if (nt + 25 <= kFastTiles) {
+        uint64_t* ft = reinterpret_cast<uint64_t*>(G);
+        for (int i = tid; i < nt + 25; i += kDtThreads) {
+          int ti, tj;
+          if (i < nt) {
+            const int r = i / nbc;
+            ti = ti0 + r;
+            tj = tj0 + (i - r * nbc);
+          } else {
+            const int r = (i - nt) / 5;
+            ti = rti0 + r;
+            tj = rtj0 + (i - nt - 5 * r);
+          }
+          uint64_t t = (ti >= 0 && ti < s.TR && tj >= 0 && tj < s.TC) ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
+          const int rows = s.Wp - 8 * ti;  // the transform reads map rows < Wp only
+          if (rows < 8) t &= rows > 0 ? low_mask(8 * rows) : 0ull;
+          ft[i] = t;
+        }
+        __syncthreads();
+        uint32_t mykey = 0;
+        for (int k = tid; k < ccnt; k += kDtThreads) {
+          const int32_t cw = s.dist_cc[(size_t)ea * kDistK + k];
+          const int cx = witness_x(cw), cy = witness_y(cw);
+          int d = s.dist_cd[(size_t)ea * kDistK + k];
+          for (int i = 0; i < nt; ++i) {
+            const int r = i / nbc;
+            d = tile_min_dist(ft[i], 8 * (ti0 + r), 8 * (tj0 + i - r * nbc), cx, cy, d);
+          }
+          s_cdv[k] = d;
+          mykey = max(mykey, ((uint32_t)d << 16) | (uint32_t)k);
+        }
+        mykey = wave_max_u32(mykey);
+        if ((tid & 63) == 0) atomicMax(&s_fkey, mykey);
+        for (int t = tid; t < T; t += kDtThreads) {
+          int tu, tv;
+          target(t, tu, tv);
+          const int tx = tu - pad, ty = tv - pad;  // map coordinates
+          int d = kInf;
+          for (int i = 0; i < 25; ++i) {
+            const int r = i / 5;
+            d = tile_min_dist(ft[nt + i], 8 * (rti0 + r), 8 * (rtj0 + i - 5 * r), tx, ty, d);
+          }
+          s_d[t] = d;
+          // exact only if no cell outside the 40 x 40 block can be nearer
+          const int b = min(min(tx - 8 * rti0, 8 * rti0 + 39 - tx), min(ty - 8 * rtj0, 8 * rtj0 + 39 - ty)) + 1;
+          if (d > b) s_ffail = 1;
+        }
+        __syncthreads();
+        fast = s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
+      }
+    }
+    const int nstrips_all = (RY + kStrip - 1) / kStrip;
+    if (!fast) {
+      for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
+      {
+        // the agent's tiles (coalesced loads) scattered as row bytes into map
+        // rows in the strip area (free until the strips start): byte tj of map
+        // row X = row X & 7 of tile (X >> 3, tj); the bytes past the last tile
+        // column are zeroed by their row's thread.  Then the extended rows:
+        // map columns shifted right by pad (a funnel shift of two words)
+        uint8_t* crow = reinterpret_cast<uint8_t*>(G);
+        const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
+        const int RB = RWm * 8;           // bytes per map row
 #pragma unroll 4
-      for (int i = tid; i < s.MT; i += kDtThreads) {
-        const uint64_t t = free_t[i];
-        const int blk = i >> 4, bi = blk / s.TCS, bj = blk - bi * s.TCS;
-        const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
-        if (ti < s.TR && tj < s.TC) {
+        for (int i = tid; i < s.MT; i += kDtThreads) {
+          const uint64_t t = free_t[i];
+          const int blk = i >> 4, bi = blk / s.TCS, bj = blk - bi * s.TCS;
+          const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
+          if (ti < s.TR && tj < s.TC) {
 #pragma unroll
-          for (int r = 0; r < 8; ++r)
-            if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(t >> (8 * r));
+            for (int r = 0; r < 8; ++r)
+              if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(t >> (8 * r));
+          }
         }
+        for (int X = tid; X < s.Wp; X += kDtThreads)
+          for (int b = s.TC; b < RB; ++b) crow[(size_t)X * RB + b] = 0;
+        __syncthreads();
+        const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
+        int any = 0;
+        for (int i = tid; i < RX * RW; i += kDtThreads) {
+          const int u = i / RW, w = i - u * RW, X = u - pad;
+          uint64_t c = 0;
+          if (X >= 0 && X < s.Wp) {  // map columns [64 w - pad, 64 w - pad + 64)
+            const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
+            const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
+            const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
+            c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
+          }
+          c &= (w == RW - 1) ? last : ~0ull;
+          Cb[i] = c;
+          any |= c != 0;
+        }
+        if (any) s_cov = 1;
       }
-      for (int X = tid; X < s.Wp; X += kDtThreads)
-        for (int b = s.TC; b < RB; ++b) crow[(size_t)X * RB + b] = 0;
       __syncthreads();
-      const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
-      int any = 0;
-      for (int i = tid; i < RX * RW; i += kDtThreads) {
-        const int u = i / RW, w = i - u * RW, X = u - pad;
-        uint64_t c = 0;
-        if (X >= 0 && X < s.Wp) {  // map columns [64 w - pad, 64 w - pad + 64)
-          const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
-          const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
-          const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
-          c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
-        }
-        c &= (w == RW - 1) ? last : ~0ull;
-        Cb[i] = c;
-        any |= c != 0;
-      }
-      if (any) s_cov = 1;
     }
-    __syncthreads();
-    const bool cov = s_cov != 0;
+    const bool cov = fast || s_cov != 0;
 
     // row-pass registers: a thread owns rows tid and tid + kDtThreads
     int lastL[2] = {-kInf, -kInf};  // last covered column left of the strip
@@ -229,8 +352,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // chunks inside it keep their d in the strip for the target reads
     const int tu_lo = min(px - 1, px + pad - s.ego), tu_hi = max(px + 1, px + pad + s.ego);
     const int tv_lo = min(py - 1, py + pad - s.ego), tv_hi = max(py + 1, py + pad + s.ego);
-    const int nstrips = cov ? (RY + kStrip - 1) / kStrip : 0;
-    for (int st = 0; st < nstrips; ++st) {
+    // one strip: thr < 0 -- the transform pass (keys, targets, strip maxima);
+    // thr >= 0 -- the cache pass (cells with d >= thr into the LDS list)
+    auto strip = [&](int st, int thr) {
       const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
       // ---- row pass: g of the strip's 32 cells of row u, as 16 u16 pairs
 #pragma unroll
@@ -341,6 +465,29 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         khi = max(khi, (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
       }
       const int v = c0 + 2 * pair;
+      if (thr >= 0) {  // the cache pass: cells with d >= thr
+#pragma unroll
+        for (int i = 0; i < kCL; ++i) {
+          const uint32_t d = __builtin_bit_cast(uint32_t, tp[i]);
+          const int dl = (int)(d & 0xFFFFu), dh = (int)(d >> 16);
+          const bool row_in = (rowmask >> i) & 1u;
+          if (row_in && v < RY && dl >= thr) {
+            const int idx = atomicAdd(&s_ccount, 1);
+            if (idx < kDistK) {
+              s_ccell[idx] = pack_witness(u0 + i - pad, v - pad);
+              s_cdv[idx] = dl;
+            }
+          }
+          if (row_in && v + 1 < RY && dh >= thr) {
+            const int idx = atomicAdd(&s_ccount, 1);
+            if (idx < kDistK) {
+              s_ccell[idx] = pack_witness(u0 + i - pad, v + 1 - pad);
+              s_cdv[idx] = dh;
+            }
+          }
+        }
+        return;
+      }
       if (v < RY && klo > bestkey) {
         bestkey = klo;
         bestv = v;
@@ -348,6 +495,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (v + 1 < RY && khi > bestkey) {
         bestkey = khi;
         bestv = v + 1;
+      }
+      if (s.dist_ch && st < kMaxTrack) {  // the strip's max(d), for the cache pass
+        const uint32_t sm2 = wave_max_u32(max(v < RY ? klo >> 16 : 0u, v + 1 < RY ? khi >> 16 : 0u));
+        if ((tid & 63) == 0) atomicMax(&s_smax[st], (int)sm2);
       }
       const bool keep = v + 1 >= tv_lo && v <= tv_hi && u0 + kCL > tu_lo && u0 <= tu_hi;
       if (keep) {  // the target cells of this chunk's columns, from registers
@@ -362,12 +513,14 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           }
         }
       }
-    }
+    };
+    const int nstrips = (cov && !fast) ? nstrips_all : 0;
+    for (int st = 0; st < nstrips; ++st) strip(st, -1);
     const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
     const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
     // witness: of the maxima, the one farthest from the robot (new coverage
     // comes from around the robot, so it keeps M valid longest)
-    if (cov && vmax >= 0) {
+    if (!fast && cov && vmax >= 0) {
       const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
       // 16 bits per field: d, far, u, v are all < 65535 (mc_create bounds
       // width + length + 4 pad), so wide grids keep an exact witness
@@ -377,11 +530,56 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     __syncthreads();
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
-    const int M = cov ? (int)(s_key >> 48) : -1;
+    const int M = fast ? (int)(s_fkey >> 16) : (cov ? (int)(s_key >> 48) : -1);
     const float Mf = (float)M;
-    if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
-      const int wu = (int)((s_key >> 16) & 0xFFFF), wv = (int)(s_key & 0xFFFF);
-      reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
+    if (fast) {
+      const int kb = (int)(s_fkey & 0xFFFFu);
+      if (tid == 0) {
+        reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, s.dist_cc[(size_t)ea * kDistK + kb]);
+        // the cached d are exact again: an empty box
+        reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(ccnt, cM0, 1 << 28, 1 << 28);
+        reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
+      }
+      for (int k = tid; k < ccnt; k += kDtThreads) s.dist_cd[(size_t)ea * kDistK + k] = s_cdv[k];
+    } else {
+      if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
+        const int wu = (int)((s_key >> 16) & 0xFFFF), wv = (int)(s_key & 0xFFFF);
+        reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
+      }
+      if (s.dist_ch) {
+        // the cache pass: every cell with d >= M - kDistT (strips whose max
+        // reaches it; the others only carry their last covered column)
+        int cnt = -1;
+        if (cov && M >= 0) {
+          const int thr = M - kDistT;
+          lastL[0] = lastL[1] = -kInf;
+          nrw[0] = nrw[1] = -1;
+          for (int st = 0; st < nstrips_all; ++st) {
+            if (st >= kMaxTrack || s_smax[st] >= thr) {
+              strip(st, thr);
+            } else {
+              const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                const int u = tid + q * kDtThreads;
+                if (u >= RX) continue;
+                const uint32_t sb = (uint32_t)(Cb[u * RW + w] >> (32 * h));
+                if (sb) lastL[q] = c0 + 31 - __clz(sb);
+              }
+            }
+          }
+          __syncthreads();
+          cnt = s_ccount <= kDistK ? s_ccount : -1;
+        }
+        for (int k = tid; k < (cnt > 0 ? cnt : 0); k += kDtThreads) {
+          s.dist_cc[(size_t)ea * kDistK + k] = s_ccell[k];
+          s.dist_cd[(size_t)ea * kDistK + k] = s_cdv[k];
+        }
+        if (tid == 0) {
+          reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(cnt, M, 1 << 28, 1 << 28);
+          reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
+        }
+      }
     }
     if (post) {
       float* dst = dist_obs + (size_t)ea * E * E;

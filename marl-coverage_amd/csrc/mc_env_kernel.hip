@@ -1617,6 +1617,15 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     L.dm[C.sub] = mw.x;
     L.dw[C.sub] = mw.y;
   }
+  // dist_reward top-cell cache: count and box of agent C.sub's cache (the
+  // box grows by this step's sensing window, mc_internal.h State::dist_ch)
+  int4 chd = make_int4(-1, 0, 0, 0);
+  int2 chb = make_int2(0, 0);
+  if (s.dist_ch && C.sub < N) {
+    const int4* hp = reinterpret_cast<const int4*>(s.dist_ch + ((size_t)e * N + C.sub) * 8);
+    chd = hp[0];
+    chb = *reinterpret_cast<const int2*>(hp + 1);
+  }
   if (fan) {
     int4* dst = reinterpret_cast<int4*>(L.fan);
     if (C.sub < n16) dst[C.sub] = fv0;
@@ -1783,6 +1792,16 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     if (s.dist && C.sub < N &&
         (reset_req || sent_reset || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
+    if (s.dist_ch && C.sub < N) {
+      int* hp = s.dist_ch + ((size_t)e * N + C.sub) * 8;
+      if (reset_req || sent_reset || L.sc->do_reset) {
+        hp[0] = -1;  // the map was cleared: the cached cells' d are stale
+      } else if (chd.x > 0) {  // every newly covered cell lies in the sensing window
+        const int x = L.x[C.sub], y = L.y[C.sub], H = s.H;
+        *reinterpret_cast<int4*>(hp) = make_int4(chd.x, chd.y, min(chd.z, x - H), min(chd.w, y - H));
+        *reinterpret_cast<int2*>(hp + 4) = make_int2(max(chb.x, x + H), max(chb.y, y + H));
+      }
+    }
   }
   STAMP(8);
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&

@@ -114,6 +114,16 @@ struct State {
   // sets M = -1 when sensing covers a cell closer than M to the witness (or
   // the env resets); otherwise M is unchanged (mc_dist.hip).
   int32_t* dist_mw;
+  // dist_reward top-cell cache (mc_dist.hip; null when off, e.g. with map
+  // sharing): per map kDistK cells (witness packing) and their d, and a
+  // header [8]: count (-1: none), M0 (max(d) when the cells were taken),
+  // the box (x0, y0, x1, y1, map coordinates) that holds every cell covered
+  // since the cells' d were last made exact (x1 < x0: empty).  The cells are
+  // every cell with d >= M0 - kDistT then; the env kernel grows the box by
+  // each step's sensing windows and drops the cache on a reset.
+  int32_t* dist_cc;
+  int32_t* dist_cd;
+  int32_t* dist_ch;
   // episode record, written when an env reports done (before an auto-reset
   // clears the counters): percent_covered() and _currstep at the end
   double* ep_pc;
@@ -121,6 +131,8 @@ struct State {
 };
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
+constexpr int kDistK = 128;          // top-cell cache: cells per map
+constexpr int kDistT = 8;            // ... with d >= M0 - kDistT
 
 // word index of tile (ti, tj) in a map (0 <= ti < 4*TRS, 0 <= tj < 4*TCS)
 __host__ __device__ inline uint32_t tile_index(int TCS, int ti, int tj) {

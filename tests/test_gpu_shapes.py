@@ -153,6 +153,38 @@ def test_c5_shape_512_per_step(torch_cuda):
     run_against_oracle(torch, env, cfg, rs, 30, sample, 5, "c5_512", dist_check=True, sentinel_p=0.0)
 
 
+def test_c5_top_cell_cache_is_exact(torch_cuda, monkeypatch):
+    """The dist_reward top-cell cache (mc_dist.hip: the cells with d >= M - 8
+    and the box of cells covered since) against the full transform
+    (MARLCOV_DIST_CACHE=0): 64 C5 envs x 120 steps of the same device
+    actions, auto-resets every 45 steps, give bit-identical obs, rewards,
+    dones and (max d, witness distance) -- max d is exact whichever path
+    made it; the per-step oracle check is test_c5_shape_512_per_step."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=45)
+    B = 64
+    outs = []
+    for cache in ("1", "0"):
+        monkeypatch.setenv("MARLCOV_DIST_CACHE", cache)
+        env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
+                                       seed=5, auto_reset=True)
+        assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+        env.reset()
+        acc = []
+        for t in range(120):
+            obs, rew, done = env.step(env.random_actions(777, t))
+            mw = env.get_state(_lib.FIELD_DIST_MW)[..., 0]
+            acc.append((obs.clone(), env.dist_obs.clone(), rew.clone(), done.clone(), mw.clone()))
+        outs.append(acc)
+    for t, (a, b) in enumerate(zip(*outs)):
+        for x, y, name in zip(a[:4], b[:4], ("obs", "dist_obs", "reward", "done")):
+            assert torch.equal(x, y), f"step {t}: {name}"
+        known = (a[4] >= 0) & (b[4] >= 0)  # max d of the maps both handles know
+        assert torch.equal(a[4][known], b[4][known]), f"step {t}: max_d"
+
+
 @pytest.mark.parametrize("rows,rx", [(600, 606), (538, 544)], ids=["rx606_kcl26", "rx544_kcl17_full"])
 def test_dist_kernel_long_maps(torch_cuda, rows, rx):
     """Extended maps of 545..832 rows run the transform as dist_kernel_t<26>
