@@ -86,23 +86,26 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--sq", action="store_true")
     ap.add_argument("--limit", type=int, default=240)
+    ap.add_argument("--analyze-only", action="store_true", help="re-summarise the runs already under --out")
     args = ap.parse_args()
     out = args.out or os.path.join(ROOT, "gpurun_out", f"prof_{args.config}")
     os.makedirs(out, exist_ok=True)
     bench = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--config", args.config,
              "--steps", str(args.steps), "--warmup", str(args.warmup)] + args.extra.split()
     os.environ.setdefault("TMPDIR", "/tmp")
-    run(bench, os.path.join(out, "bench.json"), args.limit)
-    prof = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(out, "trace"), "-o", "run",
-            "--output-format", "csv", "--"]
-    run(prof + bench, os.path.join(out, "trace.log"), args.limit)
     passes = [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]
     if args.sq:
         passes += [("pmc_sq1", SQ1), ("pmc_sq2", SQ2)]
-    for d, counters in passes:
-        cmd = ["rocprofv3", "--pmc", *counters.split(), "--kernel-trace", "-d", os.path.join(out, d), "-o", "run",
-               "--output-format", "csv", "--"]
-        run(cmd + bench, os.path.join(out, d + ".log"), args.limit)
+    if not args.analyze_only:
+        run(bench, os.path.join(out, "bench.json"), args.limit)
+        prof = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(out, "trace"), "-o", "run",
+                "--output-format", "csv", "--"]
+        run(prof + bench, os.path.join(out, "trace.log"), args.limit)
+        for d, counters in passes:
+            cmd = ["rocprofv3", "--pmc", *counters.split(), "--kernel-trace", "-d", os.path.join(out, d), "-o",
+                   "run", "--output-format", "csv", "--"]
+            run(cmd + bench, os.path.join(out, d + ".log"), args.limit)
+    passes = [p for p in passes if os.path.isdir(os.path.join(out, p[0]))]
 
     K = args.steps
     tr = trace(os.path.join(out, "trace"))
@@ -113,8 +116,10 @@ def main():
             counters.setdefault(k, {}).setdefault(d, lst)
     step = collections.defaultdict(float)
     for k, durs in tr.items():
-        if len(durs) < K or "random_actions" in k:
-            continue  # not a per-step kernel of the timed region (setup, grids, resets, action staging)
+        # a per-step kernel runs in every warmup and timed step; the rest are
+        # setup (grids, allocation fills), resets or action staging
+        if len(durs) < K + args.warmup or "random_actions" in k or k.startswith("__amd_rocclr"):
+            continue
         timed = durs[-K:]
         ent = {"dispatches_total": len(durs), "timed_dispatches": K,
                "mean_us": round(statistics.mean(timed), 3), "median_us": round(statistics.median(timed), 3)}
