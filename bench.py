@@ -344,6 +344,10 @@ def main():
                      "measured_traffic": measured},
         "cpu_baseline": cpu,
     }
+    if dr and achieved > HBM_PEAK_GBS:
+        line["roofline"]["frac_note"] = (
+            "above 1 because the 8(d) bytes price a full-map read per agent and step; the witness and "
+            "top-cell cache skip most of them (DESIGN.md §3), so measured_traffic.frac is the physical HBM fraction")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -131,8 +131,14 @@ struct State {
 };
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
-constexpr int kDistK = 128;          // top-cell cache: cells per map
-constexpr int kDistT = 8;            // ... with d >= M0 - kDistT
+#ifndef MC_DIST_K  // build-time A/B knobs (tools/build_variants.py)
+#define MC_DIST_K 256
+#endif
+#ifndef MC_DIST_T
+#define MC_DIST_T 16
+#endif
+constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
+constexpr int kDistT = MC_DIST_T;    // ... with d >= M0 - kDistT
 
 // word index of tile (ti, tj) in a map (0 <= ti < 4*TRS, 0 <= tj < 4*TCS)
 __host__ __device__ inline uint32_t tile_index(int TCS, int ti, int tj) {
