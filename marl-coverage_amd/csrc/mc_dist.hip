@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   __shared__ int s_ccount;
   __shared__ int s_smax[kMaxTrack];
   __shared__ int32_t s_ccell[kDistK];
-  __shared__ int s_cdv[kDistK];
+  __shared__ uint16_t s_cdv[kDistK];  // d < 0xFFFF (the transform saturates there)
   const int tid = threadIdx.x;
   const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad, RW = (RY + 63) >> 6;
   const int E = s.E;

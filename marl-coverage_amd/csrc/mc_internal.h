@@ -132,10 +132,10 @@ struct State {
 
 constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 #ifndef MC_DIST_K  // build-time A/B knobs (tools/build_variants.py)
-#define MC_DIST_K 256
+#define MC_DIST_K 512
 #endif
 #ifndef MC_DIST_T
-#define MC_DIST_T 16
+#define MC_DIST_T 20
 #endif
 constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
 constexpr int kDistT = MC_DIST_T;    // ... with d >= M0 - kDistT
