@@ -163,9 +163,29 @@ def cpu_baseline(cfgname, procs, secs):
     port = ("oracle/super_ref.py (SuperGridRL step restated, per-cell Python sense loop kept)"
             if CONFIGS[cfgname].get("env") == "super" else
             "oracle/cpu_ref.py (reference step restated, per-cell Python beam march kept)")
-    return {"value": round(rate, 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x {secs:.1f} s, one env each, {CONFIGS[cfgname]['desc']}, "
-                      f"random joint actions; {port}; host CPU: {cpu}"}
+    out = {"value": round(rate, 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
+           "sample": f"{procs} processes x {secs:.1f} s, one env each, {CONFIGS[cfgname]['desc']}, "
+                     f"random joint actions; {port}; host CPU: {cpu}"}
+    ratio = port_over_reference(cfgname)
+    if ratio:  # the port's rate over the reference's own step, same core (build container)
+        out["port_over_reference"] = ratio
+        out["reference_equiv_value"] = round(rate / ratio, 2)
+        out["calibration"] = CALIBRATION
+    return out
+
+
+CALIBRATION = "profiles/r4/cpu_calibration.json"
+
+
+def port_over_reference(cfgname):
+    """tools/calibrate_cpu.py: the oracle's single-core rate over the imported
+    reference DecGridRL.step's on one core of the build container, same grid,
+    actions and seeds (the reference cannot travel to the GPU box)."""
+    try:
+        with open(os.path.join(ROOT, CALIBRATION)) as f:
+            return json.load(f)["results"][cfgname]["port_over_reference"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def load_traffic(cfgname):
@@ -195,9 +215,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--maxsteps", type=int, default=None,
                     help="episode length (auto-reset on done); default: the config's (1000, C5 2000)")
-    ap.add_argument("--launch", default="stream", choices=["stream", "graph", "events"],
-                    help="stream: K back-to-back launches; graph: uploaded hipGraph replay; "
-                         "events: per-launch HIP events")
+    ap.add_argument("--launch", default="native", choices=["native", "stream", "graph", "events"],
+                    help="native: the K launches issued by one C-ABI call (mc_step_many, one kernel "
+                         "launch per step); stream: K back-to-back Python/ctypes mc_step calls; graph: "
+                         "uploaded hipGraph replay; events: per-launch HIP events")
     ap.add_argument("--eager", action="store_true", help="alias of --launch events")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI).  gloo rehearses the "
@@ -278,8 +299,10 @@ def main():
     torch.cuda.synchronize(dev)
     env.check()
 
-    elapsed, kern_ms = timed_launches(lambda i, st: env.step_raw(actions[W + i].data_ptr(), rp, dp, op, st),
-                                      dev, K, args.launch)
+    astride = B * N
+    elapsed, kern_ms, issue_us = timed_launches(
+        lambda i, st: env.step_raw(actions[W + i].data_ptr(), rp, dp, op, st), dev, K, args.launch,
+        many_fn=lambda n, st: env.step_many_raw(actions[W].data_ptr(), astride, n, rp, dp, op, st))
     env.check()
     listed = dj_listed = None
     if dr:  # maps the last step sent to the full distance transform (diagnostic)
@@ -326,7 +349,8 @@ def main():
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions; Philox keyed by "
                 "global env id)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": total_envs,
-                   "launch": LAUNCH_DESC[args.launch], "kernel_variant": env.kernel_variant(),
+                   "launch": LAUNCH_DESC[args.launch], "host_issue_us_per_step": issue_us,
+                   "kernel_variant": env.kernel_variant(),
                    **dist_desc(args, world),
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
                    "episode_phase": f"timed steps {W + 1}..{W + K} after the first reset (auto-reset at maxsteps)",
@@ -369,11 +393,14 @@ def dist_desc(args, world):
     return d
 
 
-def timed_launches(step_fn, dev, K, launch):
+def timed_launches(step_fn, dev, K, launch, many_fn=None):
     """Time K launches between barrier + synchronize; returns (elapsed s, ms
-    per launch from HIP events on the launch stream).
+    per launch from HIP events on the launch stream, host issue time per
+    step in us: from the first event record to the last launch returned).
 
-    launch = "stream": the K launches are issued back to back on the stream
+    launch = "native": one C-ABI call issues the K launches (many_fn(K,
+    stream): mc_step_many, one env-kernel launch per step, no Python or
+    ctypes per step).  "stream": the K launches are issued back to back on the stream
     (asynchronous; the host stays ahead of a ~10 us kernel, so the GPU runs
     them back to back and the first kernel starts at once).  "graph": they
     are captured into hipGraphs (chunks of 100) that are instantiated and
@@ -427,25 +454,32 @@ def timed_launches(step_fn, dev, K, launch):
             starts[i].record(stream)
             step_fn(i, stream.cuda_stream)
             ends[i].record(stream)
+    elif launch == "native":
+        rc = many_fn(K, stream.cuda_stream)
+        assert rc == 0, rc
     else:
         for i in range(K):
             step_fn(i, stream.cuda_stream)
+    t_issue = time.perf_counter()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    issue_us = round((t_issue - t0) / K * 1e6, 3)
     if launch == "events":
-        return t1 - t0, sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K
-    return t1 - t0, ev0.elapsed_time(ev1) / K
+        return t1 - t0, sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K, issue_us
+    return t1 - t0, ev0.elapsed_time(ev1) / K, issue_us
 
 
 KERNEL_US_FROM = {
+    "native": "HIP events around the K launches of one mc_step_many call / K (includes kernel boundaries)",
     "stream": "HIP events around the K back-to-back launches / K (includes kernel boundaries)",
     "graph": "HIP events around the replayed launches / K (includes kernel boundaries)",
     "events": "per-launch HIP events",
 }
-LAUNCH_DESC = {"stream": "back-to-back stream launches", "graph": "hipGraph replay (uploaded)",
+LAUNCH_DESC = {"native": "one env-kernel launch per step, the K launches issued by one mc_step_many call",
+               "stream": "back-to-back stream launches (one Python/ctypes mc_step call per step)", "graph": "hipGraph replay (uploaded)",
                "events": "stream launches with per-launch events"}
 
 
@@ -476,8 +510,9 @@ def bench_super(args, c, B, cpu, world, rank, dev, run):
         assert env.step_raw(actions[i].data_ptr(), rp, dp, sp) == 0, env.lib.mc_last_error()
     torch.cuda.synchronize(dev)
     env.check()
-    elapsed, step_ms = timed_launches(lambda i, st: env.step_raw(actions[Wm + i].data_ptr(), rp, dp, st),
-                                      dev, K, args.launch)
+    launch = "stream" if args.launch == "native" else args.launch  # (no mc_sg_step_many)
+    elapsed, step_ms, issue_us = timed_launches(lambda i, st: env.step_raw(actions[Wm + i].data_ptr(), rp, dp, st),
+                                                dev, K, launch)
     env.check()
     stats = torch.stack([env.reward.sum(), env.done.to(torch.float64).sum()])
     stats, elapsed = reduce_run(stats, elapsed, world)
@@ -503,7 +538,8 @@ def bench_super(args, c, B, cpu, world, rank, dev, run):
         "vs_baseline": None, "dtype": "f64+u64+f32",
         "data": "synthetic (device Bernoulli p_obst=0.1 grids, uniform random actions)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": run["total_envs"],
-                   "launch": LAUNCH_DESC[args.launch], **dist_desc(args, world),
+                   "launch": LAUNCH_DESC[launch], "host_issue_us_per_step": issue_us,
+                   **dist_desc(args, world),
                    "parallelism": f"env-shard x{world}",
                    "auto_reset": True, "maxsteps": args.maxsteps},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -512,7 +548,7 @@ def bench_super(args, c, B, cpu, world, rank, dev, run):
                                           "changed region (whole layer when max(d) changes)",
                      "kernel": "mcs::sg_step_kernel + mcs::sg_erode_kernel (one step)",
                      "kernel_us": round(step_ms * 1e3, 3),
-                     "kernel_us_from": KERNEL_US_FROM[args.launch] + " (both kernels of a step)",
+                     "kernel_us_from": KERNEL_US_FROM[launch] + " (both kernels of a step)",
                      "full_refresh_bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
     }

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 6
+#define MARLCOV_ABI_VERSION 7
 
 enum {
   MC_OK = 0,
@@ -145,7 +145,11 @@ enum {
   MC_FIELD_DJ_LISTED = 18,   /* int32 [1] (env, agent) paths the last step sent
                                 to the full-map BFS: nearest unexplored cell
                                 more than 24 steps away (read-only diagnostic) */
-  MC_FIELD_COUNT = 19
+  /* dist_reward configs only:                                                 */
+  MC_FIELD_DIST_CACHED = 19, /* int32 [1] of the maps the last POST listed, those
+                                the top-cell cache served without a full
+                                transform (read-only diagnostic)               */
+  MC_FIELD_COUNT = 20
 };
 
 int32_t mc_abi_version(void);
@@ -209,6 +213,20 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos,
  * episode; MC_FIELD_EP_PC / EP_LEN keep the finished episode's record. */
 int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward,
             uint8_t* dev_done, void* dev_obs, uint8_t* dev_adj, void* stream);
+
+/* num_steps consecutive mc_step calls in one call: step k reads the action
+ * bytes at dev_actions + k * actions_stride and writes reward / done / obs /
+ * adjacency at their pointer + k * stride (byte strides; 0 = every step
+ * overwrites the same buffer; dev_adj may be NULL).  Each step is launched
+ * exactly as mc_step launches it (one env-kernel launch, plus the dist /
+ * dijkstra launches of the config), stream-ordered.  For callers whose
+ * actions are known ahead (open-loop rollouts, benchmarks): one FFI crossing
+ * instead of num_steps.  Same semantics as the reference's step
+ * (dec_grid_rl.py:91-169) applied num_steps times. */
+int mc_step_many(void* env, const uint8_t* dev_actions, int64_t actions_stride, int32_t num_steps,
+                 double* dev_reward, int64_t reward_stride, uint8_t* dev_done, int64_t done_stride,
+                 void* dev_obs, int64_t obs_stride, uint8_t* dev_adj, int64_t adj_stride,
+                 void* stream);
 
 /* Device-to-device copy of a state field into / out of caller memory.
  * `bytes` must equal the field size (mc_field_bytes). */

@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
@@ -21,7 +21,7 @@ ACT_NOOP = 4
 (FIELD_POS, FIELD_MOVED, FIELD_FREE, FIELD_OBST, FIELD_VISITED, FIELD_FREE_COUNT,
  FIELD_VISITED_COUNT, FIELD_CURRSTEP, FIELD_DONE_THRESH, FIELD_ENV_GRID, FIELD_EPISODE,
  FIELD_NUMFREE, FIELD_GRID_NEG, FIELD_GRID_POS, FIELD_DIST_MW, FIELD_DIST_LISTED, FIELD_EP_PC,
- FIELD_EP_LEN, FIELD_DJ_LISTED) = range(19)
+ FIELD_EP_LEN, FIELD_DJ_LISTED, FIELD_DIST_CACHED) = range(20)
 
 
 class McConfig(ctypes.Structure):
@@ -135,6 +135,7 @@ SIGNATURES = [
     ("mc_kernel_variant", ctypes.c_char_p, [_VP]),
     ("mc_reset", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("mc_step", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("mc_step_many", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _I64, _VP]),
     ("mc_field_bytes", _I64, [_VP, _I32]),
     ("mc_get_state", ctypes.c_int, [_VP, _I32, _VP, _I64, _VP]),
     ("mc_set_state", ctypes.c_int, [_VP, _I32, _VP, _I64, _VP]),

@@ -26,6 +26,7 @@ _FIELD_DTYPES = {
     _lib.FIELD_NUMFREE: "int32", _lib.FIELD_GRID_NEG: "int64", _lib.FIELD_GRID_POS: "int64",
     _lib.FIELD_DIST_MW: "int32", _lib.FIELD_DIST_LISTED: "int32",
     _lib.FIELD_EP_PC: "float64", _lib.FIELD_EP_LEN: "int32", _lib.FIELD_DJ_LISTED: "int32",
+    _lib.FIELD_DIST_CACHED: "int32",
 }
 
 
@@ -255,6 +256,41 @@ class BatchCoverageEnv:
             return (self.obs, self.adj), self.reward, self.done
         return self.obs, self.reward, self.done
 
+    def rollout(self, actions):
+        """Step K times with known actions, one C-ABI call (mc_step_many):
+        ``actions`` uint8 [K, B, N] device tensor; returns new tensors obs
+        [K, B, N, Lc, E, E], reward [K, B], done [K, B] -- step k's outputs,
+        exactly what K ``step`` calls would have returned.  (The adjacency
+        and the float dist / minimap layers keep only the last step's.)"""
+        torch = self._torch
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.dtype == torch.uint8 and a.device == self.device
+                and a.is_contiguous()):
+            a = torch.as_tensor(a, device=self.device).to(torch.uint8).contiguous()
+        if a.dim() != 3 or tuple(a.shape[1:]) != (self.num_envs, self.num_agents):
+            raise ValueError(f"actions must be [K, {self.num_envs}, {self.num_agents}] uint8")
+        K = a.shape[0]
+        obs = torch.empty((K,) + tuple(self.obs.shape), dtype=torch.uint8, device=self.device)
+        rew = torch.empty((K, self.num_envs), dtype=torch.float64, device=self.device)
+        done = torch.empty((K, self.num_envs), dtype=torch.uint8, device=self.device)
+        if K == 0:
+            return obs, rew, done
+        _lib.check(self.lib.mc_step_many(self._h, a.data_ptr(), a[0].numel(), K, rew.data_ptr(), rew[0].numel() * 8,
+                                         done.data_ptr(), done[0].numel(), obs.data_ptr(), obs[0].numel(),
+                                         self._adj_ptr(), 0, self._stream()), "mc_step_many")
+        self.obs.copy_(obs[-1])
+        self.reward.copy_(rew[-1])
+        self.done.copy_(done[-1])
+        return obs, rew, done
+
+    def step_many_raw(self, actions_ptr: int, actions_stride: int, num_steps: int, reward_ptr: int,
+                      done_ptr: int, obs_ptr: int, stream: int):
+        """Benchmarks: ``num_steps`` launches in one C call (mc_step_many),
+        actions at ``actions_ptr + k * actions_stride``, every step's outputs
+        into the same buffers."""
+        return self.lib.mc_step_many(self._h, actions_ptr, actions_stride, num_steps, reward_ptr, 0, done_ptr, 0,
+                                     obs_ptr, 0, None, 0, stream)
+
     def random_actions(self, seed, step, out=None):
         """uint8 [B, N] actions uniform in {0..3} from Philox(seed, global env
         id, step) (mc_random_actions): the same bytes for an env whatever the
@@ -286,6 +322,7 @@ class BatchCoverageEnv:
             _lib.FIELD_GRID_NEG: (G,) + mw, _lib.FIELD_GRID_POS: (G,) + mw,
             _lib.FIELD_DIST_MW: (B, N, 2), _lib.FIELD_DIST_LISTED: (1,),
             _lib.FIELD_EP_PC: (B,), _lib.FIELD_EP_LEN: (B,), _lib.FIELD_DJ_LISTED: (1,),
+            _lib.FIELD_DIST_CACHED: (1,),
         }[field]
 
     def get_state(self, field, out=None):

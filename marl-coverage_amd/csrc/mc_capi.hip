@@ -33,6 +33,7 @@ hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float*
 hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
                             uint32_t* list, uint32_t* count, hipStream_t stream);
 size_t dist_lds_bytes(const State& s, int pad);
+size_t dist_static_lds_bytes();
 int dist_max_rows();
 size_t dijkstra_lds_bytes(const State& s, int pad);
 hipError_t launch_minimap(const State& s, int mini, double* out, hipStream_t stream);
@@ -76,7 +77,7 @@ struct Env {
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
   double* mini_obs = nullptr; // mini_map_rad: caller's float64 [B][N][2][E][E]
-  uint32_t* dist_list = nullptr;  // dist_reward: count, workgroups done, last count + [B*N] maps (full transform)
+  uint32_t* dist_list = nullptr;  // dist_reward: count, workgroups done, last count, cache hits, last hits + [B*N] maps (full transform)
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
@@ -113,6 +114,7 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_GRID_POS: return {(void*)s.grid_pos, G * mw * 8};
     case MC_FIELD_DIST_MW: return {s.dist_mw, s.dist_mw ? B * N * 8 : -1};
     case MC_FIELD_DIST_LISTED: return {E->dist_list ? E->dist_list + 2 : nullptr, E->dist_list ? 4 : -1};
+    case MC_FIELD_DIST_CACHED: return {E->dist_list ? E->dist_list + 4 : nullptr, E->dist_list ? 4 : -1};
     case MC_FIELD_EP_PC: return {s.ep_pc, B * 8};
     case MC_FIELD_EP_LEN: return {s.ep_len, B * 4};
     case MC_FIELD_DJ_LISTED: return {E->dj_list ? E->dj_list + 2 : nullptr, E->dj_list ? 4 : -1};
@@ -374,7 +376,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     int maxlds = 0;
     if (hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) !=
             hipSuccess ||
-        need + 4096 + 1024 > (size_t)maxlds) {
+        need + mc::dist_static_lds_bytes() + 1024 > (size_t)maxlds) {
       mc_destroy(E);
       return fail(MC_EINVAL, "dist_reward: %zu B of LDS bitboards for a %dx%d grid exceed the "
                   "device's %d B per workgroup", need, c.width, c.length, maxlds);
@@ -392,7 +394,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     // work list of the full transform and its count
     void *mw = nullptr, *lq = nullptr;
     if (dev_alloc(E, &mw, (size_t)s.B * s.N * 8) != MC_OK ||
-        dev_alloc(E, &lq, ((size_t)s.B * s.N + 3) * 4) != MC_OK ||
+        dev_alloc(E, &lq, ((size_t)s.B * s.N + 5) * 4) != MC_OK ||
         hipMemset(mw, 0xFF, (size_t)s.B * s.N * 8) != hipSuccess) {
       std::string msg = g_err;
       mc_destroy(E);
@@ -660,10 +662,18 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     }
   }
   HIP_TRY(hipSetDevice(E->device));
+  // a queued launch (on any stream) may still read the tables: let it finish
+  // before they are overwritten or freed.  Until the new tables are complete
+  // the handle has none (a failure below leaves mc_step refusing to run
+  // rather than reading freed or half-written tables).
+  HIP_TRY(hipDeviceSynchronize());
+  E->beams_set = false;
+  E->s.fan_nsec = E->s.fan_nspec = E->s.fan_kt = E->s.fan_words = 0;
+  E->s.fan_data = nullptr;
   if (num_beams != E->beam_count || !E->beams_buf) {
     // the reference lets callers swap _thetalist after construction
     // (even beam counts): (re-)size the device tables
-    HIP_TRY(hipDeviceSynchronize());
+    E->beam_count = 0;
     if (E->beams_buf) (void)hipFree(E->beams_buf);
     if (E->bits_buf) (void)hipFree(E->bits_buf);
     E->beams_buf = E->bits_buf = nullptr;
@@ -711,7 +721,6 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
       on = false;
     if (on) {
       if (fd.size() > E->fan_cap) {
-        HIP_TRY(hipDeviceSynchronize());
         if (E->fan_buf) (void)hipFree(E->fan_buf);
         E->fan_buf = nullptr;
         E->fan_cap = 0;
@@ -720,11 +729,11 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
       }
       HIP_TRY(hipMemcpy(E->fan_buf, fd.data(), fd.size() * 4, hipMemcpyHostToDevice));
       E->s.fan_data = (const uint32_t*)E->fan_buf;
+      E->s.fan_nsec = nsec;
+      E->s.fan_nspec = nspec;
+      E->s.fan_kt = kmax;
+      E->s.fan_words = (int)fd.size();
     }
-    E->s.fan_nsec = on ? nsec : 0;
-    E->s.fan_nspec = on ? nspec : 0;
-    E->s.fan_kt = on ? kmax : 0;
-    E->s.fan_words = on ? (int)fd.size() : 0;
   }
   E->beams_set = true;
   return MC_OK;
@@ -820,7 +829,7 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
 static int dist_terms(Env* E, int post, hipStream_t st) {
   if (!E->cfg.dist_reward) return MC_OK;
   if (post)  // window search per map, full transform for the maps whose max(d) may have changed
-    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 3,
+    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 5,
                                  E->dist_list, st));
   else
     HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, 0, E->dist_pre, E->dist_obs, st));
@@ -852,15 +861,10 @@ int mc_reset(void* env, const uint8_t* dev_env_mask, const int32_t* dev_pos, voi
   return dist_terms(E, 1, (hipStream_t)stream);
 }
 
-int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
-            void* dev_obs, uint8_t* dev_adj, void* stream) {
-  Env* E = as_env(env);
-  if (!E || !dev_actions || !dev_reward || !dev_done || !dev_obs)
-    return fail(MC_EINVAL, "mc_step: null argument");
-  int rc = ready(E, "mc_step");
-  if (rc) return rc;
-  hipStream_t st = (hipStream_t)stream;
-  HIP_TRY(hipSetDevice(E->device));
+// the launches of one step (the caller checked the arguments and set the device)
+static int step_once(Env* E, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
+                     void* dev_obs, uint8_t* dev_adj, hipStream_t st) {
+  int rc;
   if (E->cfg.map_sharing) HIP_TRY(mc::launch_share(E->s, dev_actions, st));
   if (E->cfg.map_sharing || E->dist_pre_stale) {
     rc = dist_terms(E, 0, st);  // observe() reads the maps before sensing
@@ -871,6 +875,40 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* 
   rc = dijkstra_layer(E, dev_obs, st);
   if (rc) return rc;
   return dist_terms(E, 1, st);
+}
+
+int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward, uint8_t* dev_done,
+            void* dev_obs, uint8_t* dev_adj, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_actions || !dev_reward || !dev_done || !dev_obs)
+    return fail(MC_EINVAL, "mc_step: null argument");
+  int rc = ready(E, "mc_step");
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(E->device));
+  return step_once(E, dev_actions, dev_reward, dev_done, dev_obs, dev_adj, (hipStream_t)stream);
+}
+
+int mc_step_many(void* env, const uint8_t* dev_actions, int64_t actions_stride, int32_t num_steps,
+                 double* dev_reward, int64_t reward_stride, uint8_t* dev_done, int64_t done_stride,
+                 void* dev_obs, int64_t obs_stride, uint8_t* dev_adj, int64_t adj_stride, void* stream) {
+  Env* E = as_env(env);
+  if (!E || !dev_actions || !dev_reward || !dev_done || !dev_obs)
+    return fail(MC_EINVAL, "mc_step_many: null argument");
+  if (num_steps < 0 || actions_stride < 0 || reward_stride < 0 || done_stride < 0 || obs_stride < 0 ||
+      adj_stride < 0)
+    return fail(MC_EINVAL, "mc_step_many: negative step count or stride");
+  int rc = ready(E, "mc_step_many");
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(E->device));
+  hipStream_t st = (hipStream_t)stream;
+  for (int32_t k = 0; k < num_steps; ++k) {
+    rc = step_once(E, dev_actions + k * actions_stride,
+                   reinterpret_cast<double*>(reinterpret_cast<char*>(dev_reward) + k * reward_stride),
+                   dev_done + k * done_stride, static_cast<char*>(dev_obs) + k * obs_stride,
+                   dev_adj ? dev_adj + k * adj_stride : nullptr, st);
+    if (rc) return rc;
+  }
+  return MC_OK;
 }
 
 int64_t mc_field_bytes(void* env, int32_t f) {
@@ -898,7 +936,7 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   FieldDesc d = field(E, f);
   if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
   if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED || f == MC_FIELD_EP_PC || f == MC_FIELD_EP_LEN ||
-      f == MC_FIELD_DJ_LISTED)
+      f == MC_FIELD_DJ_LISTED || f == MC_FIELD_DIST_CACHED)
     return fail(MC_EINVAL, "field %d is derived state (read-only)", f);
   if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   HIP_TRY(hipSetDevice(E->device));

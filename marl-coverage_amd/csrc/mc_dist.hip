@@ -466,6 +466,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       }
       const int v = c0 + 2 * pair;
       if (thr >= 0) {  // the cache pass: cells with d >= thr
+        // an overflowed list (count > kDistK) is dropped whole: no more atomics
+        if (*reinterpret_cast<volatile int*>(&s_ccount) > kDistK) return;
 #pragma unroll
         for (int i = 0; i < kCL; ++i) {
           const uint32_t d = __builtin_bit_cast(uint32_t, tp[i]);
@@ -535,6 +537,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     if (fast) {
       const int kb = (int)(s_fkey & 0xFFFFu);
       if (tid == 0) {
+        atomicAdd(count + 3, 1u);  // maps the cache served (MC_FIELD_DIST_CACHED)
         reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, s.dist_cc[(size_t)ea * kDistK + kb]);
         // the cached d are exact again: an empty box
         reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(ccnt, cM0, 1 << 28, 1 << 28);
@@ -594,15 +597,17 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // count[0] = entries, count[1] = workgroups done: the last workgroup to
   // finish zeroes both for the next step's window search (every workgroup has
   // read the entry count before it counts itself done; no memset launch per
-  // step) and keeps the entry count in count[2] (MC_FIELD_DIST_LISTED)
+  // step) and keeps the entry count in count[2] (MC_FIELD_DIST_LISTED); the
+  // cache hits count[3] go to count[4] the same way (MC_FIELD_DIST_CACHED)
   if (list && threadIdx.x == 0) {
     uint32_t* cnt = count;
     if (n_items == 0) {
-      if (blockIdx.x == 0) cnt[2] = 0;
+      if (blockIdx.x == 0) cnt[2] = cnt[4] = 0;
     } else {
       __threadfence();
       if (atomicAdd(cnt + 1, 1u) == gridDim.x - 1) {
         atomicExch(cnt + 2, atomicExch(cnt, 0u));
+        atomicExch(cnt + 4, atomicExch(cnt + 3, 0u));
         atomicExch(cnt + 1, 0u);
       }
     }
@@ -614,6 +619,12 @@ size_t dist_lds_bytes(const State& s, int pad) {
 }
 
 int dist_max_rows() { return kMaxRows; }
+
+// static LDS of dist_kernel_t beyond dist_lds_bytes: the top-cell cache list
+// (kDistK cells and d), the strip maxima and the scalars
+size_t dist_static_lds_bytes() {
+  return (size_t)kDistK * (sizeof(int32_t) + sizeof(uint16_t)) + kMaxTrack * sizeof(int) + 64;
+}
 
 // the instantiation whose register chunk holds ceil(RX / kChunks) rows
 static hipError_t launch_full(const State& s, int pad, int post, float* pre_out, float* dist_obs,

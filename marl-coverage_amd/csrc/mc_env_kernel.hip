@@ -1770,9 +1770,13 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, reset_req ? inj_pos : nullptr);
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
-    // obs of the current state only (dec_grid_rl.py:104-107,160)
+    // obs of the current state only (dec_grid_rl.py:104-107,160).  Only the
+    // old free / obstacle tiles are needed (fold / oold): no row or column
+    // plane is scattered.  With the fan march the column planes overlay
+    // fold / oold (carve), and a multi-wave slot's column-byte stores would
+    // race with another wave's stage_fold stores.
     Items<KI> I;
-    stage<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
+    stage_load<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
     stage_fold<NT, EPW, WT, KI>(s, C, I);
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;

@@ -82,29 +82,42 @@ class LidarRef:
         self._table = lidar_beam_table(self._thetalist)
 
     def getMeasurement(self, x, y, oc, free_map, obst_map, pad):
-        """``lidar.py:16-65``: copy both maps, march every beam."""
-        width, length = oc.shape
-        new_free = free_map.copy()
-        new_obst = obst_map.copy()
+        """``lidar.py:16-65``: copy both maps, march every beam.  The beam
+        increments are derived per call from the angle, as the reference does
+        (``:38-48``; the same expressions as ``lidar_beam_table``, so the same
+        bits), and the bound test is a method call (``:67-68``): the port's
+        per-step cost stays the reference's (the bench's CPU baseline,
+        ``tools/calibrate_cpu.py``)."""
+        width, length = np.shape(oc)
+        new_free = np.copy(free_map)
+        new_obst = np.copy(obst_map)
         rng = self._max_range
-
-        def inside(px, py):  # lidar.py:67-68
-            return px >= 0 and py >= 0 and px < width and py < length
-
-        for xinc, yinc, dinc in self._table:
+        inside = self.inbounds
+        for theta in self._thetalist:
             px = x
             py = y
+            xinc = np.cos(theta)
+            yinc = np.sin(theta)
+            larger = max(abs(xinc), abs(yinc))
+            xinc /= larger
+            yinc /= larger
+            dinc = np.sqrt(xinc ** 2 + yinc ** 2)
             travelled = 0
-            while inside(px, py) and oc[int(px), int(py)] >= 0 and travelled < rng:
+            while inside(px, py, length, width) and oc[int(px), int(py)] >= 0 and travelled < rng:
                 new_free[int(px) + pad, int(py) + pad] = 1
                 px += xinc
                 py += yinc
                 travelled += dinc
-            if inside(px, py) and oc[int(px), int(py)] >= 0:
+            if inside(px, py, length, width) and oc[int(px), int(py)] >= 0:
                 new_free[int(px) + pad, int(py) + pad] = 1
             else:
                 new_obst[int(px) + pad, int(py) + pad] = 1
         return new_free, new_obst
+
+    @staticmethod
+    def inbounds(px, py, length, width):
+        """``lidar.py:67-68``."""
+        return px >= 0 and py >= 0 and px < width and py < length
 
 
 class SquareRef:

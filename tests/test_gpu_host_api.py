@@ -102,3 +102,43 @@ def test_beam_table_over_lds_budget_is_rejected(torch_cuda):
     # the shared sensor's two envs see the same cells after the rejection
     assert env.obs.cpu().numpy().tobytes() == other.obs.cpu().numpy().tobytes()
     assert len(env.sensor._listeners) == 2
+
+
+def test_rollout_matches_steps_and_oracle(torch_cuda):
+    """mc_step_many (BatchCoverageEnv.rollout): K steps in one C-ABI call give
+    step k's obs / reward / done exactly as K mc_step calls do, and as the
+    oracle's K steps (dec_grid_rl.py:91-169), auto-resets included; the env
+    state after the rollout equals the stepped env's."""
+    import marlcov
+    from marlcov import _lib
+    from gpu_util import compare_env, device_state, oracle_from_device, ref_action
+    torch = torch_cuda
+    c = cfg(numrobot=3, maxsteps=9)
+    rs = np.random.RandomState(99)
+    B, K = 8, 24
+    grids = [np.where(rs.rand(20, 20) < 0.15, -1.0, 1.0) for _ in range(B)]
+    envs = [marlcov.BatchCoverageEnv(c, B, grids=grids, auto_reset=True, seed=3) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    acts = rs.randint(0, 4, size=(K, B, 3)).astype(np.uint8)
+    acts[rs.rand(K, B) < 0.1, 0] = 255
+    st = device_state(envs[0])
+    refs = [oracle_from_device(st, b, c) for b in range(B)]
+    obs_r, rew_r, done_r = envs[0].rollout(torch.from_numpy(acts).to(envs[0].device))
+    for k in range(K):
+        o, r, d = envs[1].step(torch.from_numpy(acts[k]).to(envs[1].device))
+        assert torch.equal(o, obs_r[k]) and torch.equal(r, rew_r[k]) and torch.equal(d, done_r[k]), k
+        for b in range(B):
+            oo, rr, dd = refs[b].step(ref_action(acts[k, b]))
+            assert float(rr) == float(rew_r[k, b]) and bool(dd) == bool(done_r[k, b]), (k, b)
+            if dd:
+                p = envs[1].get_state(_lib.FIELD_POS).cpu().numpy()[b]  # the stepped env, after step k
+                oo, _ = refs[b].reset(False, None, positions=[tuple(q) for q in p])
+            np.testing.assert_array_equal(obs_r[k, b].cpu().numpy(), oo, err_msg=f"k={k} b={b}")
+    st0, st1 = device_state(envs[0]), device_state(envs[1])
+    for b in range(B):
+        compare_env(st0, b, refs[b], f"rollout end env {b}")
+        compare_env(st1, b, refs[b], f"stepped end env {b}")
+    assert int(done_r.sum()) >= B  # maxsteps 9 over 24 steps
+    for e in envs:
+        e.check()

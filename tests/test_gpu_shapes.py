@@ -131,6 +131,78 @@ def test_c4_shape_256_many_envs(torch_cuda, monkeypatch, march):
     assert resets >= B
 
 
+def test_c4_shape_sentinels_and_partial_resets(torch_cuda):
+    """The env kernel's non-stepping branch at the C4 compiled shape (four
+    waves per env, fan march on): a sentinel row without auto_reset
+    (dec_grid_rl.py:104-107: reward 0, done, no state change, obs of the
+    current state) and every env left out of a partial mc_reset take it.
+    16 envs x 40 steps with sentinel rows at 30 %, plus partial resets with
+    an env mask at t = 12 (injected start cells) and t = 27 (device draw), each
+    step against the oracle.  Round 3's record: the column-plane scatter of
+    this branch raced with another wave's fold / oold stores (wrong obs)."""
+    import marlcov
+    from marlcov import streams
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=8, allow_even_beams=True, sensor_config={"num_lasers": 360, "range": 20})
+    rs = np.random.RandomState(4040)
+    B, N, T = 16, 8, 40
+    grids = [bern(rs, 72, 72, 0.1) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=False, seed=9)
+    assert ",C4>" in env.kernel_variant() and "+fan(" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    st = device_state(env)
+    refs = [oracle_from_device(st, b, cfg) for b in range(B)]
+    sentinels = 0
+    for t in range(T):
+        if t in (12, 27):
+            mask = rs.rand(B) < 0.5
+            mask[t % B] = True
+            mask[(t + 1) % B] = False
+            inject = t == 12
+            pos = None
+            if inject:
+                pos = st["pos"].copy()
+                for b in np.flatnonzero(mask):
+                    g = refs[b]._grid
+                    cells = np.argwhere(g >= 0)
+                    pick = cells[rs.choice(len(cells), N, replace=False)]
+                    pos[b] = pick
+            obs = env.reset(env_mask=mask.astype(np.uint8), positions=pos)
+            obs_h = full_obs(env, obs, cfg)
+            st = device_state(env)
+            for b in range(B):
+                tag = f"c4 partial reset t={t} env {b}"
+                if mask[b]:
+                    p = st["pos"][b]
+                    if inject:
+                        np.testing.assert_array_equal(p, pos[b], err_msg=tag)
+                    else:
+                        want = streams.start_cells(9, b, int(st["episode"][b]), refs[b]._grid, N)
+                        np.testing.assert_array_equal(p, want, err_msg=tag + " start cells vs host Philox")
+                    o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in p])
+                else:
+                    o = refs[b].get_egocentric_observations()
+                np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+                compare_env(st, b, refs[b], tag)
+        acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+        acts[rs.rand(B, N) < 0.06] = 9
+        sent = rs.rand(B) < 0.3
+        acts[sent, 0] = 255
+        sentinels += int(sent.sum())
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"c4 sentinel t={t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            assert bool(d) == bool(done_h[b]), tag
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+    assert sentinels >= B * T // 5
+    env.check()
+
+
 def test_c5_shape_512_per_step(torch_cuda):
     """BASELINE configs[4] geometry (16 agents, 512x512, dist_reward) on 256
     envs through the C5 instantiation: 8 envs compared with the oracle every
@@ -154,18 +226,21 @@ def test_c5_shape_512_per_step(torch_cuda):
 
 
 def test_c5_top_cell_cache_is_exact(torch_cuda, monkeypatch):
-    """The dist_reward top-cell cache (mc_dist.hip: the cells with d >= M - 8
-    and the box of cells covered since) against the full transform
-    (MARLCOV_DIST_CACHE=0): 64 C5 envs x 120 steps of the same device
-    actions, auto-resets every 45 steps, give bit-identical obs, rewards,
-    dones and (max d, witness distance) -- max d is exact whichever path
-    made it; the per-step oracle check is test_c5_shape_512_per_step."""
+    """The dist_reward top-cell cache (mc_dist.hip: the cells with d >= M -
+    kDistT, T = 20, and the box of cells covered since) against the full
+    transform (MARLCOV_DIST_CACHE=0): 64 C5 envs x 120 steps of the same
+    device actions, auto-resets every 45 steps, give bit-identical obs,
+    rewards, dones and (max d, witness distance) -- max d is exact whichever
+    path made it.  The cache handle must have served listed maps
+    (MC_FIELD_DIST_CACHED); the oracle checks of the cache are
+    test_c5_cache_steady_state_matches_oracle and test_c5_shape_512_per_step."""
     import marlcov
     from marlcov import _lib
     torch = torch_cuda
     cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=45)
     B = 64
     outs = []
+    served = {}
     for cache in ("1", "0"):
         monkeypatch.setenv("MARLCOV_DIST_CACHE", cache)
         env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
@@ -173,16 +248,69 @@ def test_c5_top_cell_cache_is_exact(torch_cuda, monkeypatch):
         assert ",C5>" in env.kernel_variant(), env.kernel_variant()
         env.reset()
         acc = []
+        served[cache] = 0
         for t in range(120):
             obs, rew, done = env.step(env.random_actions(777, t))
             mw = env.get_state(_lib.FIELD_DIST_MW)[..., 0]
+            served[cache] += int(env.get_state(_lib.FIELD_DIST_CACHED).item())
             acc.append((obs.clone(), env.dist_obs.clone(), rew.clone(), done.clone(), mw.clone()))
         outs.append(acc)
+    assert served["1"] > 0 and served["0"] == 0, served
     for t, (a, b) in enumerate(zip(*outs)):
         for x, y, name in zip(a[:4], b[:4], ("obs", "dist_obs", "reward", "done")):
             assert torch.equal(x, y), f"step {t}: {name}"
         known = (a[4] >= 0) & (b[4] >= 0)  # max d of the maps both handles know
         assert torch.equal(a[4][known], b[4][known]), f"step {t}: max_d"
+
+
+def test_c5_cache_steady_state_matches_oracle(torch_cuda, monkeypatch):
+    """The top-cell cache where the C5 bench line gets its speed: 256 C5 envs
+    (16 agents, 512 x 512, dist_reward, 2000-step episodes) run 600 device
+    random-action steps; 6 envs are then rebuilt in the oracle from device
+    state (oracle_from_device) and 25 more steps are compared with it every
+    step -- reward (float32 distance terms), done, obs with the float distance
+    layer, maps, counters -- and every known (max d, witness) against a fresh
+    transform (check_dist_mw; dec_grid_rl.py:222-223,239-240,260-282).  Most
+    of the maps those steps list for the full transform must be served by the
+    cache fast path (MC_FIELD_DIST_CACHED / MC_FIELD_DIST_LISTED)."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    monkeypatch.setenv("MARLCOV_DIST_CACHE", "1")
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=2000)
+    B = 256
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
+                                   seed=5, auto_reset=True)
+    assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    for t in range(600):
+        env.step(env.random_actions(4242, t))
+    env.check()
+    sample = [3, 40, 97, 128, 190, 251]
+    st = device_state(env, sample)
+    assert all(int(st["currstep"][b]) == 600 for b in sample)
+    refs = {b: oracle_from_device(st, b, cfg) for b in sample}
+    listed = cached = 0
+    rs = np.random.RandomState(600)
+    for t in range(25):
+        acts = rs.randint(0, 4, size=(B, 16)).astype(np.uint8)
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        listed += int(env.get_state(_lib.FIELD_DIST_LISTED).item())
+        cached += int(env.get_state(_lib.FIELD_DIST_CACHED).item())
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env, sample)
+        for b in sample:
+            o, r, d = refs[b].step(ref_action(acts[b]))
+            tag = f"c5 steady t={601 + t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            assert bool(d) == bool(done_h[b]), tag
+            if d:  # covered: the device reset the env in the same launch
+                o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in st["pos"][b]])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, refs[b], tag)
+        check_dist_mw(env, refs, f"c5 steady t={601 + t}", envs=sample)
+    assert listed > 0 and 2 * cached > listed, (listed, cached)
+    env.check()
 
 
 @pytest.mark.parametrize("rows,rx", [(600, 606), (538, 544)], ids=["rx606_kcl26", "rx544_kcl17_full"])

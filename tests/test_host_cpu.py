@@ -81,6 +81,7 @@ def test_create_rejects_bad_config(lib, bad, msg):
 def test_null_arguments_are_errors(lib):
     assert lib.mc_create(None, 0, None) == -1
     assert lib.mc_step(None, None, None, None, None, None, None) == -1
+    assert lib.mc_step_many(None, None, 0, 1, None, 0, None, 0, None, 0, None, 0, None) == -1
     assert lib.mc_reset(None, None, None, None, None, None) == -1
     assert lib.mc_query(None, None) == -1
 
