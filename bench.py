@@ -188,14 +188,34 @@ def port_over_reference(cfgname):
         return None
 
 
-def load_traffic(cfgname):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (if any)."""
+def load_traffic(cfgname, full=False):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (if any);
+    full=True: the whole record (bytes, the profiled step time and phase)."""
     path = os.path.join(ROOT, "profiles", f"traffic_{cfgname}.json")
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
     except (OSError, ValueError):
         return None
+    return rec if full else rec.get("hbm_bytes_per_launch")
+
+
+def measured_traffic(cfgname, warmup, steps):
+    """The HBM bytes a timed step really moves (PMC passes, profiles/
+    traffic_<config>.json) over the step time of the SAME profiled run (same
+    build, same episode phase), with the phase it was taken in; `matches`
+    says whether this bench run times the same phase."""
+    rec = load_traffic(cfgname, full=True)
+    if not rec or not rec.get("hbm_bytes_per_launch") or not rec.get("step_mean_us"):
+        return None
+    b, us = rec["hbm_bytes_per_launch"], rec["step_mean_us"]
+    w, k = rec.get("warmup"), rec.get("steps")
+    return {"bytes_per_step": b, "step_us": us, "achieved": round(b / (us * 1e-6) / 1e9, 2),
+            "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+            "phase": f"steps {w + 1}..{w + k} after the first reset" if w is not None and k else "unrecorded",
+            "matches_this_run": w == warmup if w is not None else None,
+            "from": f"profiles/traffic_{cfgname}.json (FETCH_SIZE x2 + WRITE_SIZE per timed step, "
+                    "rocprofv3 kernel means of the same run)"}
 
 
 def main():
@@ -299,10 +319,13 @@ def main():
     torch.cuda.synchronize(dev)
     env.check()
 
+    # every launch argument resolved before the timed region
     astride = B * N
+    aptrs = [actions[W + i].data_ptr() for i in range(K)]
+    a0 = aptrs[0] if K else 0
     elapsed, kern_ms, issue_us = timed_launches(
-        lambda i, st: env.step_raw(actions[W + i].data_ptr(), rp, dp, op, st), dev, K, args.launch,
-        many_fn=lambda n, st: env.step_many_raw(actions[W].data_ptr(), astride, n, rp, dp, op, st))
+        lambda i, st: env.step_raw(aptrs[i], rp, dp, op, st), dev, K, args.launch,
+        many_fn=lambda n, st: env.step_many_raw(a0, astride, n, rp, dp, op, st))
     env.check()
     listed = dj_listed = None
     if dr:  # maps the last step sent to the full distance transform (diagnostic)
@@ -326,14 +349,7 @@ def main():
                                          if dr else (DJ_WINDOW_CELLS if dj else 0))
     achieved = bpe * B / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
-    # the HBM bytes one step really moves (PMC passes over the timed steps,
-    # profiles/traffic_<config>.json) over the same step time: a second,
-    # separately labelled fraction (C5's 8(d) bytes price full-map reads the
-    # witness-tracked design does not make)
-    measured = ({"bytes_per_step": traffic, "achieved": round(traffic / (kern_ms * 1e-3) / 1e9, 2),
-                 "frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                 "from": f"profiles/traffic_{args.config}.json (FETCH_SIZE x2 + WRITE_SIZE per timed step)"}
-                if traffic else None)
+    measured = measured_traffic(args.config, W, K)
     line = {
         "metric": METRIC,
         "value": round(value, 1),

@@ -30,7 +30,7 @@ hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* 
                            uint32_t* list, bool window, hipStream_t stream);
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream);
-hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
+hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* dist_obs,
                             uint32_t* list, uint32_t* count, hipStream_t stream);
 size_t dist_lds_bytes(const State& s, int pad);
 size_t dist_static_lds_bytes();
@@ -253,6 +253,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   s.mg_TW = mc::magic_div((uint32_t)TW);
   s.mg_TW2 = mc::magic_div((uint32_t)(TW * TW));
   s.ego = c.egoradius;
+  s.pad = c.pad;
   s.E = 2 * c.egoradius + 1;
   s.Lc = (c.mini_map_rad > 0 ? 5 : 3) + (c.dist_reward ? 1 : 0) + (c.dijkstra_input ? 1 : 0);
   s.dist = c.dist_reward ? 1 : 0;
@@ -402,6 +403,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     }
     E->s.dist_mw = (int32_t*)mw;
     E->dist_list = (uint32_t*)lq;
+    E->s.dist_cnt = E->dist_list;
     // the top-cell cache (mc_dist.hip), off with map sharing (other agents'
     // maps add cells outside the agent's own sensing windows) or
     // MARLCOV_DIST_CACHE=0
@@ -457,8 +459,12 @@ int mc_query(void* env, mc_layout* out) {
 // axis, major sign, minor sign; minor sign 0 counts as +), ordered by their
 // minor offsets, and cut greedily into sectors of up to kFanS beams whose
 // offsets differ by 0 or 1 between neighbours at every step, at most one
-// start-dependent beam (Beam::axis bit 1) per sector; the classes are
-// interleaved, so the sectors of one march instruction mark different lines.
+// start-dependent beam (Beam::axis bit 1) per sector.  The two classes of a
+// line (same major axis and sign, minor sign + / -) are paired: sector i of
+// each, interleaved step by step in one pair record (an empty sector pads the
+// shorter class), so one lane reads the line word once for both and marks it
+// with one OR; the pairs of the four lines are interleaved, so the pairs of
+// one march instruction mark different lines.
 // A start-dependent beam marches with its common bits except from the minor
 // starts where its own bits differ before the march ends (bits[b][start],
 // cm starts); the kernel marches those alone.  Returns false (ray march) for
@@ -503,13 +509,18 @@ static bool build_fan(const std::vector<mc::Beam>& bt, const std::vector<uint64_
     }
     most = std::max(most, secs[c].size());
   }
-  std::vector<const std::vector<int>*> order;
+  static const std::vector<int> kNone;
+  std::vector<std::pair<const std::vector<int>*, const std::vector<int>*>> order;  // (minor +, minor -)
+  int real = 0;
   for (size_t i = 0; i < most; ++i)
-    for (int c = 0; c < 8; ++c)
-      if (i < secs[c].size()) order.push_back(&secs[c][i]);
-  nsec = (int)order.size();
+    for (int m = 0; m < 4; ++m) {
+      const bool p = i < secs[2 * m].size(), q = i < secs[2 * m + 1].size();
+      if (p || q) order.push_back({p ? &secs[2 * m][i] : &kNone, q ? &secs[2 * m + 1][i] : &kNone});
+      real += (int)p + (int)q;
+    }
+  nsec = 2 * (int)order.size();  // sector slots (pairs x 2, empty ones included)
   nspec = (int)spec.size();
-  if (2 * nsec > nb || N * nspec > lanes || nspec > 255) return false;
+  if (2 * real > nb || N * nspec > lanes || nspec > 255) return false;
   out.assign(mc::kFanLutBytes / 4, 0u);
   uint8_t* lut = reinterpret_cast<uint8_t*>(out.data());
   for (int D = 0; D < 32; ++D) {
@@ -528,23 +539,36 @@ static bool build_fan(const std::vector<mc::Beam>& bt, const std::vector<uint64_
   auto cbits = [](const mc::Beam& o) {
     return ((o.axis & 1) ? (uint32_t)mc::FAN_COLS : 0u) | (o.sign < 0 ? (uint32_t)mc::FAN_NEG : 0u);
   };
-  for (const std::vector<int>* S : order) {
-    const std::vector<int>& v = *S;
-    uint32_t w0 = cbits(bt[v[0]]);
+  // word 0 of a sector: its class bits and special beam; word k: step k's
+  // entry (an empty sector: the partner's class bits, entries 0 = no beam)
+  auto desc = [&](const std::vector<int>& v, uint32_t cls) {
+    uint32_t w0 = v.empty() ? cls : cbits(bt[v[0]]);
     for (size_t j = 0; j < v.size(); ++j)
       if (bt[v[j]].axis & 2) {
         const size_t si = std::find(spec.begin(), spec.end(), v[j]) - spec.begin();
         w0 |= mc::FAN_SPECIAL | ((uint32_t)j << 3) | ((uint32_t)si << 8);
       }
-    out.push_back(w0);
+    return w0;
+  };
+  auto entry = [&](const std::vector<int>& v, int k) {
+    if (v.empty()) return 0u;
+    const int lo = off(bt[v[0]], k);
+    uint32_t D = 0, valid = 0;
+    for (size_t j = 0; j < v.size(); ++j) {
+      if (j + 1 < v.size() && off(bt[v[j + 1]], k) != off(bt[v[j]], k)) D |= 1u << j;
+      if (bt[v[j]].K >= k) valid |= 1u << j;
+    }
+    return (uint32_t)(lo + 32) | (D << 6) | (valid << 16);
+  };
+  for (const auto& pr : order) {  // pair record: [desc+, desc-], then [entry+(k), entry-(k)] per step
+    const std::vector<int>& v0 = *pr.first;
+    const std::vector<int>& v1 = *pr.second;
+    const uint32_t cls = cbits(bt[(v0.empty() ? v1 : v0)[0]]);
+    out.push_back(desc(v0, cls));
+    out.push_back(desc(v1, cls));
     for (int k = 1; k <= kmax; ++k) {
-      const int lo = off(bt[v[0]], k);
-      uint32_t D = 0, valid = 0;
-      for (size_t j = 0; j < v.size(); ++j) {
-        if (j + 1 < v.size() && off(bt[v[j + 1]], k) != off(bt[v[j]], k)) D |= 1u << j;
-        if (bt[v[j]].K >= k) valid |= 1u << j;
-      }
-      out.push_back((uint32_t)(lo + 32) | (D << 6) | (valid << 16));
+      out.push_back(entry(v0, k));
+      out.push_back(entry(v1, k));
     }
   }
   for (int b : spec) {
@@ -828,9 +852,10 @@ static int dijkstra_layer(Env* E, void* dev_obs, hipStream_t st) {
 // the env kernel's reward) or the obs layer of the maps after it (POST)
 static int dist_terms(Env* E, int post, hipStream_t st) {
   if (!E->cfg.dist_reward) return MC_OK;
-  if (post)  // window search per map, full transform for the maps whose max(d) may have changed
-    HIP_TRY(mc::launch_dist_post(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 5,
-                                 E->dist_list, st));
+  if (post)  // the full transform of the maps the env kernel listed (unknown max(d), or a
+             // target its window search could not settle)
+    HIP_TRY(mc::launch_dist_listed(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 5,
+                                   E->dist_list, st));
   else
     HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, 0, E->dist_pre, E->dist_obs, st));
   E->dist_pre_stale = !post;  // a POST transform leaves PRE data for the next step
@@ -955,6 +980,7 @@ int mc_set_dist_obs(void* env, float* dev_dist_obs) {
   if (!E || !dev_dist_obs) return fail(MC_EINVAL, "mc_set_dist_obs: null argument");
   if (!E->cfg.dist_reward) return fail(MC_EINVAL, "mc_set_dist_obs: config has dist_reward = 0");
   E->dist_obs = dev_dist_obs;
+  E->s.dist_obs_out = dev_dist_obs;
   return MC_OK;
 }
 

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     __syncthreads();  // the LDS is reused by the next item
   }
   // count[0] = entries, count[1] = workgroups done: the last workgroup to
-  // finish zeroes both for the next step's window search (every workgroup has
+  // finish zeroes both for the next step's env kernel (every workgroup has
   // read the entry count before it counts itself done; no memset launch per
   // step) and keeps the entry count in count[2] (MC_FIELD_DIST_LISTED); the
   // cache hits count[3] go to count[4] the same way (MC_FIELD_DIST_CACHED)
@@ -660,98 +660,15 @@ hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float*
 // d only decreases and max(d) only decreases; the env kernel keeps M
 // (S.dist_mw) unless a new cell came closer than M to the witness, a cell
 // with d == M (then d(witness) is still M, and no cell exceeds M).  The
-// targets (the E x E crop and the 5 end cells of the next step) are near
-// the robot, so their d come from a bounded search: a 32 x 32 window
-// around the robot, dilated step by step as row bitboards (half a wave per
-// map, lane = window row).  d_in(t), the distance to the nearest covered
-// cell inside the window, is the true d(t) when d_in(t) <= the distance
-// b(t) from t to the nearest cell outside the window (any outside cell is
-// at least b(t) away; L1 paths inside a rectangle stay inside it).  A map
-// with an unknown M or a target the window cannot settle goes to the work
-// list of the full transform.
+// targets (the E x E crop and the 5 end cells of the next step) are near the
+// robot, so the env kernel settles their d from the agent's staged block
+// (mc_env_kernel.hip dist_window) and lists only the maps with an unknown M
+// or a target the block cannot settle; the full transform runs over that
+// list.  The list grid is fixed (hipGraph capture) and strides.
 // --------------------------------------------------------------------------
-constexpr int kLocalThreads = 256;
-constexpr int kWin = 32;
-
-__global__ __launch_bounds__(kLocalThreads) void dist_local_kernel(State s, int pad,
-                                                                   float* __restrict__ pre_out,
-                                                                   float* __restrict__ dist_obs,
-                                                                   uint32_t* __restrict__ list,
-                                                                   uint32_t* __restrict__ count) {
-  const int tid = threadIdx.x;
-  const uint32_t ea = (blockIdx.x * kLocalThreads + tid) / kWin;
-  const int r = tid & (kWin - 1);  // window row of this lane
-  const int hb = (tid & 63) & ~(kWin - 1);  // first lane of this half wave
-  if (ea >= (uint32_t)s.B * s.N) return;  // whole half waves
-  const int2 mw = reinterpret_cast<const int2*>(s.dist_mw)[ea];
-  const int M = mw.x;
-  const int E = s.E, T = 5 + E * E;
-  if (M < 0 || T > kWin) {
-    if (r == 0) list[atomicAdd(count, 1u)] = ea;
-    return;
-  }
-  const int2 p = reinterpret_cast<const int2*>(s.pos)[ea];
-  const int ti0 = (p.x - 12) >> 3, tj0 = (p.y - 12) >> 3;  // floor: window tile origin
-  const int X0 = 8 * ti0, Y0 = 8 * tj0;
-  // row r of the window: bits of tiles (ti0 + r/8, tj0 .. tj0 + 3)
-  uint32_t cur = 0;
-  {
-    const int ti = ti0 + (r >> 3);
-    const uint64_t* ft = s.freem + (size_t)ea * s.MT;
-    if (ti >= 0 && ti < s.TR) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int tj = tj0 + q;
-        if (tj >= 0 && tj < s.TC)
-          cur |= (uint32_t)((ft[tile_index(s.TCS, ti, tj)] >> (8 * (r & 7))) & 0xFFull) << (8 * q);
-      }
-    }
-  }
-  // target of this lane (map coordinates), window-local (tr, tc), bound b
-  int tx, ty;
-  if (r < 5) {  // distance_map[x, y] of the next step's end cells (quirk: no pad offset)
-    tx = p.x + (r == 1 ? 1 : (r == 3 ? -1 : 0)) - pad;
-    ty = p.y + (r == 2 ? 1 : (r == 4 ? -1 : 0)) - pad;
-  } else {
-    const int k = r < T ? r - 5 : 0, rr = k / E;
-    tx = p.x - s.ego + rr;
-    ty = p.y - s.ego + (k - rr * E);
-  }
-  const int tr = tx - X0, tc = ty - Y0;
-  const bool live = r < T;
-  const bool inwin = tr >= 0 && tr < kWin && tc >= 0 && tc < kWin;
-  const int b = inwin ? min(min(tr, kWin - 1 - tr), min(tc, kWin - 1 - tc)) + 1 : 0;
-  int dt = -1;
-  for (int k = 0; k < kWin / 2; ++k) {
-    const uint32_t row = (uint32_t)__shfl((int)cur, hb + (inwin ? tr : 0), 64);
-    if (live && inwin && dt < 0 && ((row >> tc) & 1u)) dt = k;
-    const uint64_t pend = __ballot(live && inwin && dt < 0 && k < b);
-    if (((pend >> hb) & 0xFFFFFFFFull) == 0) break;
-    const uint32_t up = (uint32_t)__shfl((int)cur, hb + (r > 0 ? r - 1 : 0), 64);
-    const uint32_t dn = (uint32_t)__shfl((int)cur, hb + (r < kWin - 1 ? r + 1 : r), 64);
-    cur |= (cur << 1) | (cur >> 1) | (r > 0 ? up : 0u) | (r < kWin - 1 ? dn : 0u);
-  }
-  const bool ok = !live || (inwin && dt >= 0 && dt <= b);
-  const uint64_t bad = __ballot(!ok);
-  if ((bad >> hb) & 0xFFFFFFFFull) {
-    if (r == 0) list[atomicAdd(count, 1u)] = ea;
-    return;
-  }
-  float* pd = pre_out + (size_t)ea * 8;
-  if (r == 0) pd[0] = (float)M;
-  if (r < 5) pd[1 + r] = (float)dt;
-  else if (live) dist_obs[(size_t)ea * E * E + (r - 5)] = dist_value((float)dt, (float)M);
-}
-
-// POST: the window search for every map, then the full transform for the
-// maps it listed.  The list grid is fixed (hipGraph capture) and strides.
-hipError_t launch_dist_post(const State& s, int pad, float* pre_out, float* dist_obs,
-                            uint32_t* list, uint32_t* count, hipStream_t stream) {
+hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* dist_obs,
+                              uint32_t* list, uint32_t* count, hipStream_t stream) {
   const size_t maps = (size_t)s.B * s.N;
-  hipLaunchKernelGGL(dist_local_kernel, dim3((unsigned)((maps * kWin + kLocalThreads - 1) / kLocalThreads)),
-                     dim3(kLocalThreads), 0, stream, s, pad, pre_out, dist_obs, list, count);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
   const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
   return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, stream);
 }

@@ -48,7 +48,7 @@ __device__ __forceinline__ int rdlane(int v, int lane) { return __builtin_amdgcn
 
 struct Scal {
   double pen;          // move penalties, accumulated in robot order
-  double done_thresh;
+  uint64_t dist_fail;  // dist_reward: agents with a target the window search left unsettled
   uint64_t moved;      // robots present in the reference's _robot_pad
   uint32_t cnt_free;   // newly set bits over all agents' free maps
   uint32_t cnt_vis;    // newly covered union cells (the obs reward)
@@ -451,14 +451,20 @@ __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW,
       // 8*ti .. 8*ti+7 of the agent's block)
       const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
+      const uint64_t ft = (known && I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
+#ifndef MC_ABL_ROWSCAT
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
-      const uint64_t ft = (known && I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
 #pragma unroll
         for (int r = 0; r < 8; ++r) fb[off + r * rs] = (uint8_t)(ft >> (8 * r));
       }
+#endif
+#ifdef MC_ABL_COLSCAT
+      if (false) {
+#else
       if (fan_on(s)) {
+#endif
         // fan march: the column planes too -- byte ti of words 8*tj .. 8*tj+7
         // are the transposed tile's bytes
         uint8_t* cb = reinterpret_cast<uint8_t*>(L.cneg);
@@ -811,11 +817,17 @@ __device__ __forceinline__ T* lds_ptr(uint32_t a) {
   return reinterpret_cast<T*>((char*)((lds_char*)(uintptr_t)a));
 }
 
-// one (agent, sector): entries T[1..kt] (T[0]: class bits), live beams A
+#ifndef MC_FAN_SU  // fan_pair's steps per batch (5: C4's 20 steps in 4 batches, 115 VGPRs; 8 needs 144)
+#define MC_FAN_SU 5
+#endif
+// one (agent, sector pair): the two sectors of one line (minor sign + / -),
+// entries T[2k], T[2k + 1] of step k (T[0], T[1]: class bits), live beams A0,
+// A1.  The line word of step k is read once for both sectors (grid cells and
+// seen cells) and their new marks go out as one OR.
 template <typename WT, int KM>
-__device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, const uint32_t* T, int a,
-                                           uint32_t A, int kt) {
-  constexpr int SU = 10;  // steps per batch: reads, then the live-beam chain, then marks
+__device__ __forceinline__ void fan_pair(const State& s, const Lds<WT>& L, const uint32_t* T, int a,
+                                         uint32_t A0, uint32_t A1, int kt) {
+  constexpr int SU = MC_FAN_SU;  // steps per batch: reads, then the live-beam chains, then marks
   const uint32_t MD = (uint32_t)(row_plane_words(s.N, s.TW, (int)sizeof(WT)) * (int)sizeof(WT));  // neg -> marks
   const uint8_t* spread = reinterpret_cast<const uint8_t*>(L.fan);
   const uint8_t* expand = spread + 2048;
@@ -827,33 +839,47 @@ __device__ __forceinline__ void fan_sector(const State& s, const Lds<WT>& L, con
   const uint32_t P0 = lds_addr(cols ? L.cneg : L.negr) + (uint32_t)row_word<WT>(s, a, cols ? ly : lx) * sizeof(WT);
   const int stride = ((desc & FAN_NEG) ? -1 : 1) * row_step<WT>(s) * (int)sizeof(WT);
   const int bb = (cols ? lx : ly) - 32;  // bit of the cell at minor offset lo: bb + (lo + 32)
+  const uint2* T2 = reinterpret_cast<const uint2*>(T);
   for (int k0 = 1; k0 <= kt; k0 += SU) {
-    uint32_t e[SU], F[SU], SN[SU], kill[SU], lit[SU];
+    uint32_t e0[SU], e1[SU], F0[SU], F1[SU], S0[SU], S1[SU];
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      e[u] = F[u] = SN[u] = 0;
+      e0[u] = e1[u] = F0[u] = F1[u] = S0[u] = S1[u] = 0;
       if (KM > 0 ? (k0 + u <= KM) : (k0 + u <= kt)) {
-        e[u] = T[k0 + u];
+        const uint2 e = T2[k0 + u];
+        e0[u] = e.x;
+        e1[u] = e.y;
         const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-        const int sh = bb + (int)(e[u] & 63u);
-        F[u] = (uint32_t)(*lds_ptr<const WT>(P) >> sh) & 63u;
-        SN[u] = (uint32_t)(*lds_ptr<const WT>(P + 2 * MD) >> sh) & 63u;
+        const WT fw = *lds_ptr<const WT>(P), sw = *lds_ptr<const WT>(P + 2 * MD);
+        const int sh0 = bb + (int)(e0[u] & 63u), sh1 = bb + (int)(e1[u] & 63u);
+        F0[u] = (uint32_t)(fw >> sh0) & 63u;
+        F1[u] = (uint32_t)(fw >> sh1) & 63u;
+        S0[u] = (uint32_t)(sw >> sh0) & 63u;
+        S1[u] = (uint32_t)(sw >> sh1) & 63u;
       }
     }
-#pragma unroll
-    for (int u = 0; u < SU; ++u) kill[u] = expand[(e[u] & 0x7C0u) | F[u]];
+    uint32_t k0v[SU], k1v[SU];
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      A &= e[u] >> 16;  // in range (a step past the trip count has e = 0)
-      lit[u] = spread[(e[u] & 0x7C0u) | A];
-      A &= ~kill[u];
+      k0v[u] = expand[(e0[u] & 0x7C0u) | F0[u]];
+      k1v[u] = expand[(e1[u] & 0x7C0u) | F1[u]];
     }
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      const uint32_t nm = lit[u] & ~SN[u];
-      if (nm) {
+      A0 &= e0[u] >> 16;  // in range (a step past the trip count, or an empty sector, has e = 0)
+      A1 &= e1[u] >> 16;
+      const uint32_t l0 = spread[(e0[u] & 0x7C0u) | A0], l1 = spread[(e1[u] & 0x7C0u) | A1];
+      A0 &= ~k0v[u];
+      A1 &= ~k1v[u];
+      F0[u] = l0 & ~S0[u];  // new marks (the cells the agent has not seen)
+      F1[u] = l1 & ~S1[u];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      if (F0[u] | F1[u]) {
         const uint32_t P = P0 + (uint32_t)((k0 + u) * stride);
-        lds_or<WT>(lds_ptr<WT>(P + MD), (WT)nm << (bb + (int)(e[u] & 63u)));
+        const WT m = ((WT)F0[u] << (bb + (int)(e0[u] & 63u))) | ((WT)F1[u] << (bb + (int)(e1[u] & 63u)));
+        lds_or<WT>(lds_ptr<WT>(P + MD), m);
       }
     }
   }
@@ -865,10 +891,11 @@ __device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>
   const Lds<WT>& L = C.L;
   const int N = s.N;
   const int kt = KM > 0 ? KM : s.fan_kt;
-  const int nsec = s.fan_nsec, nspec = s.fan_nspec;
-  const int qs = N * nsec;  // (agent, sector) lane-sectors
+  const int npair = s.fan_nsec >> 1, nspec = s.fan_nspec;
+  const int RW = 2 * (kt + 1);  // words per pair record
+  const int qs = N * npair;     // (agent, sector pair) lane items
   const uint32_t* sec = L.fan + kFanLutBytes / 4;
-  const uint32_t* sdesc = sec + nsec * (kt + 1);  // special beams: 8 words each
+  const uint32_t* sdesc = sec + npair * RW;  // special beams: 8 words each
   // special beam i of (agent, special) pairs: lane (qs + i) % LPE
   // (mc_set_beam_table keeps N * nspec <= lanes per env) loads the start word
   // of its robot's post-move cell now, for the pass after the sectors
@@ -884,30 +911,34 @@ __device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>
     if (exc) spw = (uint32_t)s.beam_bits[(size_t)d[0] * s.bcmax + c0];
   }
   for (int q = C.sub; q < qs; q += LPE) {
-    const int sg = q / N, a = q - sg * N;
-    const uint32_t* T = sec + sg * (kt + 1);
-    const uint32_t desc = T[0];
-    uint32_t A = 63u;
-    if (desc & FAN_SPECIAL) {  // the sector's special beam: left out from an exceptional start
-      const uint32_t* d = sdesc + 8 * (desc >> 8);
-      const int c0 = (desc & FAN_COLS) ? L.x[a] : L.y[a];
-      if (c0 >= (int)d[4] && c0 <= (int)d[5]) A &= ~(1u << ((desc >> 3) & 7u));
+    const int pg = q / N, a = q - pg * N;
+    const uint32_t* T = sec + pg * RW;
+    uint32_t A[2] = {63u, 63u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t desc = T[h];
+      if (desc & FAN_SPECIAL) {  // the sector's special beam: left out from an exceptional start
+        const uint32_t* d = sdesc + 8 * (desc >> 8);
+        const int c0 = (desc & FAN_COLS) ? L.x[a] : L.y[a];
+        if (c0 >= (int)d[4] && c0 <= (int)d[5]) A[h] &= ~(1u << ((desc >> 3) & 7u));
+      }
     }
-    fan_sector<WT, KM>(s, L, T, a, A, kt);
+    fan_pair<WT, KM>(s, L, T, a, A[0], A[1], kt);
   }
   if (__ballot(exc)) {  // one-beam march of the left-out beams, from the start's bits
     if (exc) {
       const int a = si / nspec;
       const uint32_t* d = sdesc + 8 * (si - a * nspec);
       const int msign = (int)d[2], K = (int)d[3];
-      uint32_t* W = L.fspec + si * (kt + 1);
-      W[0] = d[1];
+      uint32_t* W = L.fspec + si * RW;  // a pair record with an empty second sector
+      W[0] = W[1] = d[1];
       int lo = 0;
       for (int k = 1; k <= kt; ++k) {
         lo += ((spw >> (k - 1)) & 1u) ? msign : 0;
-        W[k] = (uint32_t)(lo + 32) | (K >= k ? (1u << 16) : 0u);
+        W[2 * k] = (uint32_t)(lo + 32) | (K >= k ? (1u << 16) : 0u);
+        W[2 * k + 1] = 0u;
       }
-      fan_sector<WT, KM>(s, L, W, a, 1u, kt);
+      fan_pair<WT, KM>(s, L, W, a, 1u, 0u, kt);
     }
   }
 }
@@ -1104,6 +1135,16 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       I.no[k] = op & ~o0;
       L.fold[idx] = f0 | fp;
       L.oold[idx] = o0 | op;
+      if (s.dist) {
+        // dist_reward: the post-step free tile's 8 rows into the (dead)
+        // mark-row plane, for dist_window (byte tj of block rows 8 ti ..)
+        uint8_t* rb = reinterpret_cast<uint8_t*>(L.fpr);
+        const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
+        const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);
+        const uint64_t ft = f0 | fp;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) rb[off + r * rs] = (uint8_t)(ft >> (8 * r));
+      }
       cf += __popcll(I.nf[k]);
       uint64_t cand = fp & ~u0;
       const int a = I.a[k], gi = I.gi[k], gj = I.gj[k];
@@ -1150,6 +1191,74 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
   }
   if (cf) atomicAdd(&L.sc->cnt_free, cf);
   if (cv) atomicAdd(&L.sc->cnt_vis, cv);
+}
+
+// dist_reward POST terms (dec_grid_rl.py:222-223,239-240,260-282,350-352)
+// of the agents whose max(d) M is still known (mc_dist.hip): d of each target
+// -- the 5 end cells of the next step at the quirk index (padded-grid x, y
+// read without the pad offset) and the E x E crop -- is the L1 distance to
+// the nearest covered cell of the agent's staged block (post-step free rows,
+// written into fpr by merge), exact when it does not exceed b, the distance
+// from the target to the nearest cell outside the block (any covered cell
+// there is at least b away).  Rows are scanned outward from the target's row
+// until the row distance reaches the best d.  Writes pre[e][a] (M, d of the
+// end cells) and the float obs crop; an agent with a target it cannot settle
+// is flagged in dist_fail (listed for the full transform, which rewrites its
+// terms).  `skip`: agents left to the full transform anyway.
+template <typename WT>
+__device__ __forceinline__ int row_dist(WT row, int c) {  // |c - nearest set bit|, or a large value
+  const WT lo = row & (((WT)2 << c) - (WT)1), hi = row >> c;
+  int h = 1 << 20;
+  if constexpr (sizeof(WT) == 4) {
+    if (lo) h = c - (31 - __clz((uint32_t)lo));
+    if (hi) h = min(h, __ffs((uint32_t)hi) - 1);
+  } else {
+    if (lo) h = c - (63 - __clzll((unsigned long long)lo));
+    if (hi) h = min(h, __ffsll((unsigned long long)hi) - 1);
+  }
+  return h;
+}
+
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, WT>& C, uint64_t skip) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  const int N = s.N, E = s.E, T = 5 + E * E, RB = 8 * s.TW;
+  const WT cols = sizeof(WT) == 8 && RB >= 64 ? ~(WT)0 : (WT)(((uint64_t)1 << RB) - 1);  // the block's columns
+  float* pre = const_cast<float*>(s.dist_pre);
+  for (int idx = C.sub; idx < N * T; idx += LPE) {
+    const int a = idx / T, t = idx - a * T;
+    if ((skip >> a) & 1ull) continue;
+    const int px = L.x[a], py = L.y[a];
+    int tx, ty;
+    if (t < 5) {
+      tx = px + (t == 1 ? 1 : (t == 3 ? -1 : 0)) - s.pad;
+      ty = py + (t == 2 ? 1 : (t == 4 ? -1 : 0)) - s.pad;
+    } else {
+      const int k = t - 5, r = k / E;
+      tx = px - s.ego + r;
+      ty = py - s.ego + (k - r * E);
+    }
+    const int lx = tx - 8 * L.bx[a], ly = ty - 8 * L.by[a];
+    const int b = min(min(lx, RB - 1 - lx), min(ly, RB - 1 - ly)) + 1;  // <= 0: outside the block
+    int d = b + 1;
+    if (b > 0) {
+      d = row_dist<WT>(L.fpr[row_word<WT>(s, a, lx)] & cols, ly);
+      for (int dr = 1; dr < d; ++dr) {
+        if (lx - dr >= 0) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx - dr)] & cols, ly));
+        if (lx + dr < RB) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx + dr)] & cols, ly));
+      }
+    }
+    if (d > b) {
+      atomicOr((unsigned long long*)&L.sc->dist_fail, 1ull << a);
+      continue;
+    }
+    const size_t ea = (size_t)C.e * N + a;
+    const int M = L.dm[a];
+    if (t < 5) pre[ea * 8 + 1 + t] = (float)d;
+    else s.dist_obs_out[ea * E * E + (t - 5)] = dist_value((float)d, (float)M);
+    if (t == 0) pre[ea * 8] = (float)M;
+  }
 }
 
 template <bool O32>
@@ -1598,6 +1707,8 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   const bool reset_req = valid && !is_step && req != 0;
   const bool active = valid && is_step && !sentinel;
   const bool sent_reset = sentinel && s.auto_reset;  // a sentinel's done resets too
+  // dist_reward: this lane's agent (C.sub < N) goes to the full transform's list
+  bool dlist = false;
   if (C.sub < N) {
     set_agent<WT>(s, L, C.sub, p0.x, p0.y);
     L.act[C.sub] = (uint8_t)act;
@@ -1610,6 +1721,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     L.sc->cnt_vis = 0;
     L.sc->do_reset = 0;
     L.sc->dist_hit = 0;
+    L.sc->dist_fail = 0;
     L.sc->zero = 0;
   }
   if (s.dist && C.sub < N) {  // dist_reward: M and witness of each free map
@@ -1750,6 +1862,16 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
         c->do_reset = do_reset ? 1 : 0;
       }
     }
+    // dist_reward: the POST terms of the maps whose M is still known (the
+    // others, and a reset env's, go to the full transform's list)
+    if (s.dist) {
+      uint64_t skip = L.sc->dist_hit;
+      if (do_reset) skip = ~0ull;
+      for (int i = 0; i < N && !do_reset; ++i) skip |= (uint64_t)(L.dm[i] < 0) << i;
+      dist_window<NT, EPW, WT>(s, C, skip);
+      __syncthreads();
+      dlist = C.sub < N && (((skip | L.sc->dist_fail) >> C.sub) & 1ull);
+    }
     // several waves: the slot's Scal reads above come before reset_env's
     // writes (one wave: its LDS operations complete in order)
     if constexpr (NT > 64) __syncthreads();
@@ -1768,6 +1890,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       s.ep_len[e] = currstep0;
     }
     reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, reset_req ? inj_pos : nullptr);
+    dlist = s.dist && C.sub < N;  // fresh maps: M unknown
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
     // obs of the current state only (dec_grid_rl.py:104-107,160).  Only the
@@ -1778,6 +1901,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     Items<KI> I;
     stage_load<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
     stage_fold<NT, EPW, WT, KI>(s, C, I);
+    // unchanged maps keep their dist terms; an unknown M (a state upload)
+    // needs the full transform
+    dlist = s.dist && C.sub < N && L.dm[C.sub] < 0;
     if (C.sub == 0 && sentinel) {
       reward_out[e] = 0.0;
       done_out[e] = 1;
@@ -1806,6 +1932,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
         *reinterpret_cast<int2*>(hp + 4) = make_int2(max(chb.x, x + H), max(chb.y, y + H));
       }
     }
+  }
+  if (valid && dlist) {  // the full transform's work list (mc_dist.hip launch_dist_listed)
+    const uint32_t slot = atomicAdd(s.dist_cnt, 1u);
+    s.dist_cnt[5 + slot] = (uint32_t)e * (uint32_t)N + (uint32_t)C.sub;
   }
   STAMP(8);
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&

@@ -61,6 +61,7 @@ struct State {
   int TW;                  // window tiles per side (window_tiles(H))
   uint32_t mg_TW2, mg_TW, mg_LcE, mg_E, mg_nb;  // magic reciprocals: n / d == umulhi(n, mg_d)
   int ego, E, Lc;          // egoradius, obs side, obs layers
+  int pad;                 // max(egoradius, mini_map_rad): the extended grid's ring (dec_grid_rl.py:78)
   int sensor, nbeams, sq_r;
   double pen, term, dincr;
   int maxsteps, comm_r, sst, auto_reset, grid_mode;
@@ -88,8 +89,9 @@ struct State {
   uint32_t beam_k1;
   // Fan march of a dense beam set (mc_env_kernel.hip fan_march; built by
   // mc_set_beam_table, off when fan_nsec + fan_nspec == 0).  fan_data: the
-  // spread / expand LUTs (kFanLutBytes), fan_nsec sector records of
-  // fan_kt + 1 words (word 0: FAN_* class bits, word k: step k's entry) and
+  // spread / expand LUTs (kFanLutBytes), fan_nsec / 2 sector-pair records of
+  // 2 (fan_kt + 1) words (the two sectors of one line, interleaved: words 0, 1
+  // their FAN_* class bits, words 2k, 2k + 1 their step-k entries) and
   // fan_nspec special-beam records of 8 words (FAN_SPECIAL);
   // fan_words words in all (a multiple of 4), copied into LDS each launch.
   int fan_nsec, fan_nspec, fan_kt, fan_words;
@@ -114,6 +116,12 @@ struct State {
   // sets M = -1 when sensing covers a cell closer than M to the witness (or
   // the env resets); otherwise M is unchanged (mc_dist.hip).
   int32_t* dist_mw;
+  // dist_reward POST outputs of the env kernel's window search (mc_env_kernel
+  // dist_window): the caller's float32 obs layer [B][N][E][E] and the header
+  // of the full transform's work list (count at [0], entries from [5]:
+  // mc_dist.hip dist_kernel_t)
+  float* dist_obs_out;
+  uint32_t* dist_cnt;
   // dist_reward top-cell cache (mc_dist.hip; null when off, e.g. with map
   // sharing): per map kDistK cells (witness packing) and their d, and a
   // header [8]: count (-1: none), M0 (max(d) when the cells were taken),
@@ -187,10 +195,10 @@ constexpr int kFanLutBytes = 4096;
 enum : uint32_t { FAN_COLS = 1u, FAN_NEG = 2u, FAN_SPECIAL = 4u };
 
 // LDS bytes of the fan region (replaces the beam records): the fan data and
-// the per-(agent, special beam) entries.  The fan's column planes share the
-// tile region (env_lds_bytes; mc_env_kernel.hip carve).
+// the per-(agent, special beam) pair records.  The fan's column planes share
+// the tile region (env_lds_bytes; mc_env_kernel.hip carve).
 __host__ __device__ inline size_t fan_lds_bytes(int N, int nspec, int kt, int words) {
-  return (size_t)words * 4 + (size_t)N * nspec * (kt + 1) * 4;
+  return (size_t)words * 4 + (size_t)N * nspec * 2 * (kt + 1) * 4;
 }
 
 // LDS bytes of one env slot of the env kernel (host + device use the same carve).

@@ -24,6 +24,8 @@ def main():
     total = sum(v.get("hbm_bytes", 0) for v in ks.values())
     out = {
         "config": s["config"],
+        "warmup": s["warmup"],
+        "steps": s["steps"],
         "hbm_bytes_per_launch": total,
         "per_kernel": {k: {"hbm_bytes": v.get("hbm_bytes"), "read": v.get("hbm_read_bytes"),
                            "write": v.get("hbm_write_bytes"), "mean_us": v["mean_us"]} for k, v in ks.items()},
