@@ -327,9 +327,10 @@ def main():
         lambda i, st: env.step_raw(aptrs[i], rp, dp, op, st), dev, K, args.launch,
         many_fn=lambda n, st: env.step_many_raw(a0, astride, n, rp, dp, op, st))
     env.check()
-    listed = dj_listed = None
-    if dr:  # maps the last step sent to the full distance transform (diagnostic)
+    listed = dj_listed = served = None
+    if dr:  # maps the last step sent to the full distance transform, and those the cache served (diagnostic)
         listed = int(env.get_state(marlcov._lib.FIELD_DIST_LISTED).item())
+        served = int(env.get_state(marlcov._lib.FIELD_DIST_CACHED).item())
     if dj:  # (env, agent) paths the last step sent to the full-map BFS (diagnostic)
         dj_listed = int(env.get_state(marlcov._lib.FIELD_DJ_LISTED).item())
 
@@ -370,7 +371,7 @@ def main():
                    **dist_desc(args, world),
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
                    "episode_phase": f"timed steps {W + 1}..{W + K} after the first reset (auto-reset at maxsteps)",
-                   **({"dist_full_transforms_last_step": listed} if dr else {}),
+                   **({"dist_listed_maps_last_step": listed, "dist_cache_served_last_step": served} if dr else {}),
                    **({"dijkstra_full_map_paths_last_step": dj_listed} if dj else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

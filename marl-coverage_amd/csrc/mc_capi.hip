@@ -409,10 +409,11 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     // MARLCOV_DIST_CACHE=0
     const char* dc = getenv("MARLCOV_DIST_CACHE");
     if (!c.map_sharing && !(dc && dc[0] == '0')) {
-      void *cc = nullptr, *cd = nullptr, *ch = nullptr;
+      void *cc = nullptr, *cd = nullptr, *ch = nullptr, *sm = nullptr;
       const size_t maps = (size_t)s.B * s.N;
       if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
-          dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess) {
+          dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess ||
+          dev_alloc(E, &sm, maps * mc::kDistStrips * 2) != MC_OK) {
         std::string msg = g_err;
         mc_destroy(E);
         return fail(MC_EHIP, "dist_reward cache: %s", msg.c_str());
@@ -420,6 +421,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       E->s.dist_cc = (int32_t*)cc;
       E->s.dist_cd = (int32_t*)cd;
       E->s.dist_ch = (int32_t*)ch;
+      E->s.dist_sm = (uint16_t*)sm;
     }
   }
   mc_layout& L = E->lay;
@@ -996,7 +998,7 @@ int mc_set_minimap_obs(void* env, double* dev_minimap_obs) {
 int mc_debug_stamps(void* env, uint64_t* dev_stamps) {
   Env* E = as_env(env);
   if (!E) return fail(MC_EINVAL, "mc_debug_stamps: null env");
-#ifdef MC_STAMPS
+#if defined(MC_STAMPS) || defined(MC_DIST_STAMPS)
   E->s.stamps = dev_stamps;
   return MC_OK;
 #else

@@ -46,6 +46,23 @@
 
 namespace mc {
 
+// -DMC_DIST_STAMPS diagnostic builds (tools/dist_stamps.py): per listed map
+// ea (< B * 16) one u64 in State::stamps -- cycles/16 of the staging + fast
+// path, the main strips and the cache pass (16 bits each), and flags (bit 48
+// fast path served, 49 one-pass cache list kept, 50 second cache pass ran).
+#ifdef MC_DIST_STAMPS
+#define DSTAMP(v)                                                               \
+  do {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+  } while (0)
+#else
+#define DSTAMP(v) \
+  do {            \
+  } while (0)
+#endif
+
 namespace {
 constexpr int kDtThreads = 512;
 constexpr int kStrip = 32;                     // columns per strip
@@ -59,7 +76,11 @@ constexpr int kSP = 36;
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
 constexpr int kRowOff = 1024;                  // g - u + kRowOff > 0 (u < kMaxRows)
-constexpr int kMaxTrack = 64;                  // strips whose max(d) the cache pass can skip by
+constexpr int kMaxTrack = kDistStrips;         // strips whose max(d) the cache pass can skip by
+#ifndef MC_DIST_ONEPASS  // build knob (A/B): collect the cache cells in the transform pass
+#define MC_DIST_ONEPASS 1
+#endif
+constexpr bool kOnePass = MC_DIST_ONEPASS != 0;
 constexpr int kFastTiles = 2048;               // tiles the cache fast path stages (box + 25 around the robot)
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 constexpr u16x2 kNone2 = {0xFFFF, 0xFFFF};
@@ -168,6 +189,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   __shared__ uint32_t s_fkey;
   __shared__ int s_ffail;
   __shared__ int s_ccount;
+  __shared__ int s_kept;
   __shared__ int s_smax[kMaxTrack];
   __shared__ int32_t s_ccell[kDistK];
   __shared__ uint16_t s_cdv[kDistK];  // d < 0xFFFF (the transform saturates there)
@@ -187,6 +209,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   const uint32_t n_items = list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x;
   for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
     const uint32_t ea = list ? list[it] : it;
+    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0;
+    DSTAMP(ts0);
     const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
     const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
     const int px = pp.x, py = pp.y;
@@ -211,6 +235,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       s_fkey = 0;
       s_ffail = 0;
       s_ccount = 0;
+      s_kept = 0;
     }
     for (int i = tid; i < kMaxTrack; i += kDtThreads) s_smax[i] = 0;
     // the map's top-cell cache (mc_internal.h State::dist_ch)
@@ -263,7 +288,11 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           const int32_t cw = s.dist_cc[(size_t)ea * kDistK + k];
           const int cx = witness_x(cw), cy = witness_y(cw);
           int d = s.dist_cd[(size_t)ea * kDistK + k];
-          for (int i = 0; i < nt; ++i) {
+          // every newly covered cell lies in the box: a cell at least d from
+          // the box keeps its d (the cached cells are the map's farthest from
+          // coverage, mostly far from the recent path)
+          const int bdist = max(0, max(bx0 - cx, cx - bx1)) + max(0, max(by0 - cy, cy - by1));
+          for (int i = 0; i < (bdist < d ? nt : 0); ++i) {
             const int r = i / nbc;
             d = tile_min_dist(ft[i], 8 * (ti0 + r), 8 * (tj0 + i - r * nbc), cx, cy, d);
           }
@@ -336,6 +365,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       __syncthreads();
     }
     const bool cov = fast || s_cov != 0;
+    DSTAMP(ts1);
 
     // row-pass registers: a thread owns rows tid and tid + kDtThreads
     int lastL[2] = {-kInf, -kInf};  // last covered column left of the strip
@@ -352,9 +382,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // chunks inside it keep their d in the strip for the target reads
     const int tu_lo = min(px - 1, px + pad - s.ego), tu_hi = max(px + 1, px + pad + s.ego);
     const int tv_lo = min(py - 1, py + pad - s.ego), tv_hi = max(py + 1, py + pad + s.ego);
-    // one strip: thr < 0 -- the transform pass (keys, targets, strip maxima);
+    // one strip: thr < 0 -- the transform pass (keys, targets, strip maxima;
+    // with cthr >= 0 also the cells with d >= cthr into the LDS list);
     // thr >= 0 -- the cache pass (cells with d >= thr into the LDS list)
-    auto strip = [&](int st, int thr) {
+    auto strip = [&](int st, int thr, int cthr) {
       const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
       // ---- row pass: g of the strip's 32 cells of row u, as 16 u16 pairs
 #pragma unroll
@@ -465,22 +496,23 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         khi = max(khi, (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
       }
       const int v = c0 + 2 * pair;
-      if (thr >= 0) {  // the cache pass: cells with d >= thr
-        // an overflowed list (count > kDistK) is dropped whole: no more atomics
-        if (*reinterpret_cast<volatile int*>(&s_ccount) > kDistK) return;
+      const int collect = thr >= 0 ? thr : cthr;
+      // cells with d >= collect into the LDS list; an overflowed list (count
+      // > kDistK) is dropped whole: no more atomics
+      if (collect >= 0 && *reinterpret_cast<volatile int*>(&s_ccount) <= kDistK) {
 #pragma unroll
         for (int i = 0; i < kCL; ++i) {
           const uint32_t d = __builtin_bit_cast(uint32_t, tp[i]);
           const int dl = (int)(d & 0xFFFFu), dh = (int)(d >> 16);
           const bool row_in = (rowmask >> i) & 1u;
-          if (row_in && v < RY && dl >= thr) {
+          if (row_in && v < RY && dl >= collect) {
             const int idx = atomicAdd(&s_ccount, 1);
             if (idx < kDistK) {
               s_ccell[idx] = pack_witness(u0 + i - pad, v - pad);
               s_cdv[idx] = dl;
             }
           }
-          if (row_in && v + 1 < RY && dh >= thr) {
+          if (row_in && v + 1 < RY && dh >= collect) {
             const int idx = atomicAdd(&s_ccount, 1);
             if (idx < kDistK) {
               s_ccell[idx] = pack_witness(u0 + i - pad, v + 1 - pad);
@@ -488,8 +520,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
             }
           }
         }
-        return;
       }
+      if (thr >= 0) return;
       if (v < RY && klo > bestkey) {
         bestkey = klo;
         bestv = v;
@@ -517,7 +549,51 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       }
     };
     const int nstrips = (cov && !fast) ? nstrips_all : 0;
-    for (int st = 0; st < nstrips; ++st) strip(st, -1);
+    // the cache's cells in the same pass: every cell with d >= M - kDistT
+    // (M = the new max, known only at the end) has d >= any lower bound of
+    // M, less kDistT.  Bounds: the exact current d of the cached cells (the
+    // fast path computed them before it failed) and the strips' maxima so far
+    // (s_smax two strips back: past two barriers).  The list then holds a
+    // superset, filtered at the end; without a bound (no cache tried) or on
+    // overflow, a second pass over the strips collects them.
+    const int theta0 = (s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0;
+    // Strip pruning (with that bound): a strip whose max(d) at the last full
+    // transform (State::dist_sm, an upper bound now: d only decreases) is
+    // below theta0 - kDistT holds neither the new max, nor a witness, nor a
+    // cache cell; only its rows' last covered column is carried.  The
+    // strips of the target cells always run.
+    // Strip pruning (with that bound): a strip whose max(d) at the last full
+    // transform (State::dist_sm, an upper bound now: d only decreases) is
+    // below theta0 - kDistT holds neither the new max, nor a witness, nor a
+    // cache cell; only its rows' last covered column is carried.  The
+    // strips of the target cells always run.  (Tried: strips in descending
+    // order of their bound with the exact maxima so far as the bound, a
+    // barrier per strip: slower, 263 vs 242 us per step at C5.)
+    const bool prune = theta0 > 0 && nstrips_all <= kMaxTrack;
+    const uint16_t* smb = s.dist_ch ? s.dist_sm + (size_t)ea * kMaxTrack : nullptr;
+    int runmax = 0;
+    uint64_t ran = 0;  // strips transformed (their s_smax are exact maxima)
+    for (int st = 0; st < nstrips; ++st) {
+      if (st >= 2 && st - 2 < kMaxTrack && ((ran >> (st - 2)) & 1ull)) runmax = max(runmax, s_smax[st - 2]);
+      if (prune) {
+        const int c0 = st * kStrip, bound = smb[st];
+        if (bound < theta0 - kDistT && !(c0 + kStrip > tv_lo && c0 <= tv_hi)) {
+          if (tid == 0) s_smax[st] = bound;
+          const int w = c0 >> 6, h = (c0 >> 5) & 1;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int u = tid + q * kDtThreads;
+            if (u >= RX) continue;
+            const uint32_t sb = (uint32_t)(Cb[u * RW + w] >> (32 * h));
+            if (sb) lastL[q] = c0 + 31 - __clz(sb);
+          }
+          continue;
+        }
+      }
+      ran |= 1ull << (st < 64 ? st : 63);
+      strip(st, -1, (kOnePass && theta0 > 0) ? max(theta0, runmax) - kDistT : -1);
+    }
+    DSTAMP(ts2);
     const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
     const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
     // witness: of the maxima, the one farthest from the robot (new coverage
@@ -553,13 +629,29 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         // the cache pass: every cell with d >= M - kDistT (strips whose max
         // reaches it; the others only carry their last covered column)
         int cnt = -1;
-        if (cov && M >= 0) {
+        const bool main_ok = kOnePass && theta0 > 0 && s_ccount <= kDistK;  // the main pass's list holds them all
+        if (cov && M >= 0 && main_ok) {
+          const int thr = M - kDistT, n = s_ccount;
+          for (int k = tid; k < n; k += kDtThreads)
+            if ((int)s_cdv[k] >= thr) {
+              const int j = atomicAdd(&s_kept, 1);
+              s.dist_cc[(size_t)ea * kDistK + j] = s_ccell[k];
+              s.dist_cd[(size_t)ea * kDistK + j] = s_cdv[k];
+            }
+          __syncthreads();
+          cnt = s_kept;
+          dflags |= 1ull << 49;
+        } else if (cov && M >= 0) {
+          dflags |= 1ull << 50;
+          __syncthreads();  // every thread has read s_ccount
+          if (tid == 0) s_ccount = 0;
+          __syncthreads();
           const int thr = M - kDistT;
           lastL[0] = lastL[1] = -kInf;
           nrw[0] = nrw[1] = -1;
           for (int st = 0; st < nstrips_all; ++st) {
             if (st >= kMaxTrack || s_smax[st] >= thr) {
-              strip(st, thr);
+              strip(st, thr, -1);
             } else {
               const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
 #pragma unroll
@@ -573,11 +665,16 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           }
           __syncthreads();
           cnt = s_ccount <= kDistK ? s_ccount : -1;
+          for (int k = tid; k < (cnt > 0 ? cnt : 0); k += kDtThreads) {
+            s.dist_cc[(size_t)ea * kDistK + k] = s_ccell[k];
+            s.dist_cd[(size_t)ea * kDistK + k] = s_cdv[k];
+          }
         }
-        for (int k = tid; k < (cnt > 0 ? cnt : 0); k += kDtThreads) {
-          s.dist_cc[(size_t)ea * kDistK + k] = s_ccell[k];
-          s.dist_cd[(size_t)ea * kDistK + k] = s_cdv[k];
-        }
+        // the strip maxima for the next transform's pruning (skipped strips
+        // keep their bound)
+        if (cnt > 0)
+          for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
+            s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
         if (tid == 0) {
           reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(cnt, M, 1 << 28, 1 << 28);
           reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
@@ -592,6 +689,19 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     float* pd = pre_out + (size_t)ea * 8;
     if (tid == 0) pd[0] = Mf;
     if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
+    DSTAMP(ts3);
+#ifdef MC_DIST_STAMPS
+    if (tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u) {
+      auto f16 = [](uint64_t a, uint64_t b) -> uint64_t {
+        const uint64_t d = (b - a) >> 4;
+        return d < 0xFFFFull ? d : 0xFFFFull;
+      };
+      s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, ts3) << 32) | dflags |
+                     (fast ? 1ull << 48 : 0ull);
+    }
+#else
+    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)dflags;
+#endif
     __syncthreads();  // the LDS is reused by the next item
   }
   // count[0] = entries, count[1] = workgroups done: the last workgroup to

@@ -452,19 +452,13 @@ __device__ __forceinline__ void stage_scatter(const State& s, const Ctx<NT, EPW,
       const size_t off = (size_t)row_word<WT>(s, I.a[k], 8 * I.ti[k]) * sizeof(WT) + I.tj[k];
       const size_t rs = (size_t)row_step<WT>(s) * sizeof(WT);  // one window row
       const uint64_t ft = (known && I.masks && in) ? (I.f[k] | I.o[k]) : 0ull;
-#ifndef MC_ABL_ROWSCAT
 #pragma unroll
       for (int r = 0; r < 8; ++r) nb[off + r * rs] = (uint8_t)(nt >> (8 * r));
       if (known) {  // the cells the agent has seen (old free | obstacle tiles), the same way
 #pragma unroll
         for (int r = 0; r < 8; ++r) fb[off + r * rs] = (uint8_t)(ft >> (8 * r));
       }
-#endif
-#ifdef MC_ABL_COLSCAT
-      if (false) {
-#else
       if (fan_on(s)) {
-#endif
         // fan march: the column planes too -- byte ti of words 8*tj .. 8*tj+7
         // are the transposed tile's bytes
         uint8_t* cb = reinterpret_cast<uint8_t*>(L.cneg);
@@ -1204,7 +1198,8 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
 // until the row distance reaches the best d.  Writes pre[e][a] (M, d of the
 // end cells) and the float obs crop; an agent with a target it cannot settle
 // is flagged in dist_fail (listed for the full transform, which rewrites its
-// terms).  `skip`: agents left to the full transform anyway.
+// terms).  `skip`: agents left to the full transform anyway (as is every
+// agent whose M is unknown).
 template <typename WT>
 __device__ __forceinline__ int row_dist(WT row, int c) {  // |c - nearest set bit|, or a large value
   const WT lo = row & (((WT)2 << c) - (WT)1), hi = row >> c;
@@ -1228,7 +1223,8 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
   float* pre = const_cast<float*>(s.dist_pre);
   for (int idx = C.sub; idx < N * T; idx += LPE) {
     const int a = idx / T, t = idx - a * T;
-    if ((skip >> a) & 1ull) continue;
+    const int M = L.dm[a];
+    if (((skip >> a) & 1ull) || M < 0) continue;
     const int px = L.x[a], py = L.y[a];
     int tx, ty;
     if (t < 5) {
@@ -1243,7 +1239,9 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
     const int b = min(min(lx, RB - 1 - lx), min(ly, RB - 1 - ly)) + 1;  // <= 0: outside the block
     int d = b + 1;
     if (b > 0) {
-      d = row_dist<WT>(L.fpr[row_word<WT>(s, a, lx)] & cols, ly);
+      // the target's row, then rows outward while they can help (a covered
+      // target, d = 0, is the common case next to the robot: one read)
+      d = min(d, row_dist<WT>(L.fpr[row_word<WT>(s, a, lx)] & cols, ly));
       for (int dr = 1; dr < d; ++dr) {
         if (lx - dr >= 0) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx - dr)] & cols, ly));
         if (lx + dr < RB) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx + dr)] & cols, ly));
@@ -1254,7 +1252,6 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
       continue;
     }
     const size_t ea = (size_t)C.e * N + a;
-    const int M = L.dm[a];
     if (t < 5) pre[ea * 8 + 1 + t] = (float)d;
     else s.dist_obs_out[ea * E * E + (t - 5)] = dist_value((float)d, (float)M);
     if (t == 0) pre[ea * 8] = (float)M;
@@ -1865,12 +1862,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     // dist_reward: the POST terms of the maps whose M is still known (the
     // others, and a reset env's, go to the full transform's list)
     if (s.dist) {
-      uint64_t skip = L.sc->dist_hit;
-      if (do_reset) skip = ~0ull;
-      for (int i = 0; i < N && !do_reset; ++i) skip |= (uint64_t)(L.dm[i] < 0) << i;
+      const uint64_t skip = do_reset ? ~0ull : L.sc->dist_hit;  // (and every agent with M < 0)
       dist_window<NT, EPW, WT>(s, C, skip);
       __syncthreads();
-      dlist = C.sub < N && (((skip | L.sc->dist_fail) >> C.sub) & 1ull);
+      dlist = C.sub < N && ((((skip | L.sc->dist_fail) >> C.sub) & 1ull) || L.dm[C.sub] < 0);
     }
     // several waves: the slot's Scal reads above come before reset_env's
     // writes (one wave: its LDS operations complete in order)

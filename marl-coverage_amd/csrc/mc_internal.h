@@ -132,6 +132,10 @@ struct State {
   int32_t* dist_cc;
   int32_t* dist_cd;
   int32_t* dist_ch;
+  // with the cache: per map, an upper bound of max(d) over each 32-column
+  // strip of the extended grid ([B][N][kDistStrips] u16: the strip maxima of
+  // the last full transform; d only decreases), valid while the cache is
+  uint16_t* dist_sm;
   // episode record, written when an env reports done (before an auto-reset
   // clears the counters): percent_covered() and _currstep at the end
   double* ep_pc;
@@ -146,6 +150,7 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 #define MC_DIST_T 20
 #endif
 constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
+constexpr int kDistStrips = 64;      // strips whose maxima the cache keeps (extended grids up to 2048 columns)
 constexpr int kDistT = MC_DIST_T;    // ... with d >= M0 - kDistT
 
 // word index of tile (ti, tj) in a map (0 <= ti < 4*TRS, 0 <= tj < 4*TCS)

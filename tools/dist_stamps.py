@@ -1,0 +1,73 @@
+"""Per-map phase timing of the dist_reward full-transform kernel at C5 steady
+state (diagnostic build, -DMC_DIST_STAMPS; csrc/mc_dist.hip DSTAMP).
+
+    python tools/dist_stamps.py [--envs 8192] [--warmup 600] [--build-only]
+
+Runs C5 to step `warmup`, steps once more with the stamp buffer attached and
+prints, for the maps that step listed, the staging / main-strip / cache-pass
+cycles (median, p90, max) split by path (cache fast path or full transform)
+and how the cache list was rebuilt.  Stamps perturb the schedule: read shares.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = os.path.join(ROOT, "marl-coverage_amd")
+LIB = os.path.join(PKG, "libmarlcov_dstamps.so")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=8192)
+    ap.add_argument("--warmup", type=int, default=600)
+    ap.add_argument("--build-only", action="store_true")
+    args = ap.parse_args()
+    if args.build_only:
+        sys.path.insert(0, PKG)
+        import build as mcbuild
+        mcbuild.build(extra_flags=["-DMC_DIST_STAMPS"], out=LIB)
+        return
+    os.environ["MARLCOV_LIB"] = LIB
+    import numpy as np
+    import torch
+    import marlcov
+    from marlcov import _lib
+    import bench
+
+    c = bench.CONFIGS["c5"]
+    cfg = dict(bench.BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], maxsteps=2000,
+               **c.get("extra", {}))
+    B = args.envs
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1000),
+                                   seed=1, auto_reset=True)
+    env.reset()
+    for t in range(args.warmup):
+        env.step(env.random_actions(7, t))
+    st = torch.zeros((B, 16), dtype=torch.int64, device=env.device)
+    _lib.check(env.lib.mc_debug_stamps(env._h, st.data_ptr()), "stamps")
+    env.step(env.random_actions(7, args.warmup))
+    torch.cuda.synchronize()
+    listed = int(env.get_state(_lib.FIELD_DIST_LISTED).item())
+    served = int(env.get_state(_lib.FIELD_DIST_CACHED).item())
+    s = st.cpu().numpy().reshape(-1).astype(np.uint64)
+    s = s[s != 0]
+    print(f"step {args.warmup + 1}: listed {listed}, cache served {served}, stamped {len(s)}")
+    fast = (s >> np.uint64(48)) & np.uint64(1)
+    kept = (s >> np.uint64(49)) & np.uint64(1)
+    second = (s >> np.uint64(50)) & np.uint64(1)
+    ph = [((s >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
+    for name, m in (("fast path", fast == 1), ("full, one-pass list", (fast == 0) & (kept == 1)),
+                    ("full, second pass", (fast == 0) & (second == 1)),
+                    ("full, no cache", (fast == 0) & (kept == 0) & (second == 0))):
+        if not m.any():
+            print(f"  {name:22s} n=0")
+            continue
+        row = "  ".join(f"{lab} med {np.median(p[m]):8.0f} p90 {np.percentile(p[m], 90):8.0f} max {p[m].max():8d}"
+                        for lab, p in zip(("stage", "strips", "cache"), ph))
+        print(f"  {name:22s} n={m.sum():5d}  {row}")
+
+
+if __name__ == "__main__":
+    main()

@@ -7,7 +7,7 @@ for rep in $(seq 1 ${REPS:-2}); do
   for v in ${VARIANTS}; do
     lib="$R/marl-coverage_amd/libmarlcov_v_$v.so"; [ "$v" = cur ] && lib="$R/marl-coverage_amd/libmarlcov.so"
     MARLCOV_LIB="$lib" timeout -k 10 300 python3 bench.py --no-cpu $ARGS > "$OUT/${v}_$rep.json" 2> "$OUT/${v}_$rep.err" || exit 1
-    python3 -c "import json; d=json.load(open('$OUT/${v}_$rep.json')); print('$v rep $rep', round(d['value']/1e6,3), 'M', d['roofline']['kernel_us'], 'us', d['config'].get('dist_full_transforms_last_step',''))"
+    python3 -c "import json; d=json.load(open('$OUT/${v}_$rep.json')); print('$v rep $rep', round(d['value']/1e6,3), 'M', d['roofline']['kernel_us'], 'us', d['config'].get('dist_listed_maps_last_step',''), d['config'].get('dist_cache_served_last_step',''))"
   done
 done
 exit 0
