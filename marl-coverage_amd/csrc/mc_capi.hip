@@ -31,7 +31,7 @@ hipError_t launch_dijkstra(const State& s, int pad, int layer, int Lc, uint8_t* 
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream);
 hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* dist_obs,
-                            uint32_t* list, uint32_t* count, hipStream_t stream);
+                              uint32_t* list, uint32_t* count, uint32_t* full, hipStream_t stream);
 size_t dist_lds_bytes(const State& s, int pad);
 size_t dist_static_lds_bytes();
 int dist_max_rows();
@@ -78,6 +78,7 @@ struct Env {
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
   double* mini_obs = nullptr; // mini_map_rad: caller's float64 [B][N][2][E][E]
   uint32_t* dist_list = nullptr;  // dist_reward: count, workgroups done, last count, cache hits, last hits + [B*N] maps (full transform)
+  uint32_t* dist_full = nullptr;  // with the cache: the split transform's list (mc_dist.hip mode 2)
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
   void* beams_buf = nullptr;  // mc::Beam [beam_count]
@@ -410,10 +411,13 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     const char* dc = getenv("MARLCOV_DIST_CACHE");
     if (!c.map_sharing && !(dc && dc[0] == '0')) {
       void *cc = nullptr, *cd = nullptr, *ch = nullptr, *sm = nullptr;
+      void *gk = nullptr, *gd = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr;
       const size_t maps = (size_t)s.B * s.N;
       if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
           dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess ||
-          dev_alloc(E, &sm, maps * mc::kDistStrips * 2) != MC_OK) {
+          dev_alloc(E, &sm, maps * mc::kDistStrips * 2) != MC_OK || dev_alloc(E, &gk, maps * 8) != MC_OK ||
+          dev_alloc(E, &gd, maps * 4) != MC_OK || dev_alloc(E, &gc, maps * 4) != MC_OK ||
+          dev_alloc(E, &ga, maps * 4 * mc::kDistK * 8) != MC_OK || dev_alloc(E, &fl, (maps * 2 + 8) * 4) != MC_OK) {
         std::string msg = g_err;
         mc_destroy(E);
         return fail(MC_EHIP, "dist_reward cache: %s", msg.c_str());
@@ -422,6 +426,13 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       E->s.dist_cd = (int32_t*)cd;
       E->s.dist_ch = (int32_t*)ch;
       E->s.dist_sm = (uint16_t*)sm;
+      E->s.dist_gkey = (unsigned long long*)gk;
+      E->s.dist_gdone = (uint32_t*)gd;
+      E->s.dist_gcnt = (uint32_t*)gc;
+      E->s.dist_gcand = (int2*)ga;
+      // MARLCOV_DIST_SPLIT=0: every listed map's full transform in one workgroup
+      const char* sp = getenv("MARLCOV_DIST_SPLIT");
+      if (!(sp && sp[0] == '0')) E->dist_full = E->s.dist_full = (uint32_t*)fl;
     }
   }
   mc_layout& L = E->lay;
@@ -857,7 +868,7 @@ static int dist_terms(Env* E, int post, hipStream_t st) {
   if (post)  // the full transform of the maps the env kernel listed (unknown max(d), or a
              // target its window search could not settle)
     HIP_TRY(mc::launch_dist_listed(E->s, E->cfg.pad, E->dist_pre, E->dist_obs, E->dist_list + 5,
-                                   E->dist_list, st));
+                                   E->dist_list, E->dist_full, st));
   else
     HIP_TRY(mc::launch_dist(E->s, E->cfg.pad, 0, E->dist_pre, E->dist_obs, st));
   E->dist_pre_stale = !post;  // a POST transform leaves PRE data for the next step

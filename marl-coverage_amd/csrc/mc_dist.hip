@@ -64,15 +64,21 @@ namespace mc {
 #endif
 
 namespace {
-constexpr int kDtThreads = 512;
+#ifndef MC_DT_THREADS  // build knob (A/B): threads per transform workgroup, 512 or 1024
+#define MC_DT_THREADS 512
+#endif
+constexpr int kDtThreads = MC_DT_THREADS;
+static_assert(kDtThreads == 512 || kDtThreads == 1024, "a column pair's chunks are a half wave or a wave");
 constexpr int kStrip = 32;                     // columns per strip
 constexpr int kPairs = kStrip / 2;             // column pairs (packed u16 halves) per strip
-constexpr int kCh = kDtThreads / kPairs;       // row chunks per column pair: the 32 lanes of a half wave
-// LDS stride, padded off the bank period: a strip row is 36 u16 (72 B = 18
-// dwords: the row pass's 8-byte stores of 16 consecutive rows hit 32
-// distinct banks; at 64 B four rows shared each bank; the column pass's
-// dword reads of 32 chunks 17 rows apart hit 32 distinct banks)
-constexpr int kSP = 36;
+constexpr int kCh = kDtThreads / kPairs;       // row chunks per column pair: the lanes of a half wave / a wave
+// LDS stride, padded off the bank period.  512 threads: a strip row is 36
+// u16 (72 B = 18 dwords: the row pass's 8-byte stores of 16 consecutive rows
+// hit 32 distinct banks; at 64 B four rows shared each bank; the column
+// pass's dword reads of 32 chunks 17 rows apart hit 32 distinct banks).
+// 1024 threads: 34 u16 (17 dwords, odd: 32 chunks 9 rows apart, and 16
+// consecutive rows' 8-byte stores, on distinct banks)
+constexpr int kSP = kCh == 64 ? 34 : 36;
 constexpr int kInf = 1 << 20;                  // "no covered cell in this row"
 constexpr int kMaxRows = 832;                  // RX limit of the largest instantiation
 constexpr int kRowOff = 1024;                  // g - u + kRowOff > 0 (u < kMaxRows)
@@ -94,6 +100,39 @@ template <int CTRL>
 __device__ __forceinline__ u16x2 dpp2(u16x2 v) {  // source lane out of the row: 0xFFFF pair
   return __builtin_bit_cast(u16x2, __builtin_amdgcn_update_dpp((int)0xFFFFFFFF, __builtin_bit_cast(int, v),
                                                                CTRL, 0xF, 0xF, false));
+}
+// 64 chunks (1024 threads): the whole wave, four 16-lane rows
+__device__ __forceinline__ u16x2 excl_prefix_min64(u16x2 v) {
+  const int l = threadIdx.x & 63;
+  u16x2 x = __builtin_elementwise_min(v, dpp2<0x111>(v));
+  x = __builtin_elementwise_min(x, dpp2<0x112>(x));
+  x = __builtin_elementwise_min(x, dpp2<0x114>(x));
+  x = __builtin_elementwise_min(x, dpp2<0x118>(x));  // inclusive within the row
+  const u16x2 t0 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  const u16x2 t1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 31));
+  const u16x2 t2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 47));
+  const u16x2 c1 = t0, c2 = __builtin_elementwise_min(t0, t1), c3 = __builtin_elementwise_min(c2, t2);
+  const int row = l >> 4;
+  const u16x2 carry = row == 0 ? kNone2 : (row == 1 ? c1 : (row == 2 ? c2 : c3));  // the rows before
+  u16x2 e = dpp2<0x111>(x);
+  e = (l & 15) == 0 ? kNone2 : e;
+  return __builtin_elementwise_min(e, carry);
+}
+__device__ __forceinline__ u16x2 excl_suffix_min64(u16x2 v) {
+  const int l = threadIdx.x & 63;
+  u16x2 x = __builtin_elementwise_min(v, dpp2<0x101>(v));
+  x = __builtin_elementwise_min(x, dpp2<0x102>(x));
+  x = __builtin_elementwise_min(x, dpp2<0x104>(x));
+  x = __builtin_elementwise_min(x, dpp2<0x108>(x));  // inclusive within the row, from the right
+  const u16x2 s1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 16));
+  const u16x2 s2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 32));
+  const u16x2 s3 = __builtin_bit_cast(u16x2, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 48));
+  const u16x2 c2 = s3, c1 = __builtin_elementwise_min(s2, s3), c0 = __builtin_elementwise_min(c1, s1);
+  const int row = l >> 4;
+  const u16x2 carry = row == 3 ? kNone2 : (row == 2 ? c2 : (row == 1 ? c1 : c0));  // the rows after
+  u16x2 e = dpp2<0x101>(x);
+  e = (l & 15) == 15 ? kNone2 : e;
+  return __builtin_elementwise_min(e, carry);
 }
 __device__ __forceinline__ u16x2 excl_prefix_min32(u16x2 v) {
   const int l = threadIdx.x & 63;
@@ -154,7 +193,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // rows per column chunk: the instantiation (8, 17 or 26) whose kCh chunks
 // cover RX; the strip holds kCh * chunk rows (rows >= RX are padding with
 // no covered cell)
-__host__ __device__ constexpr int chunk_rows(int RX) { return RX <= 256 ? 8 : (RX <= 544 ? 17 : 26); }
+__host__ __device__ constexpr int chunk_rows(int RX) {
+  return kCh == 64 ? (RX <= 256 ? 4 : (RX <= 576 ? 9 : 13)) : (RX <= 256 ? 8 : (RX <= 544 ? 17 : 26));
+}
 
 // LDS carve of the full transform (bytes): row bitboard | strip (u16, also the
 // tile staging area) | chunk minima | targets
@@ -175,12 +216,160 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
   return L;
 }
 
+// ---- the top-cell cache fast path of one listed map: the cells covered
+// since the cached d were exact all lie in the box, so the current d of a
+// cached cell is min(its d, the distance to the box's covered cells).  Every
+// other cell had d < M0 - kDistT when the cache was taken, and d only
+// decreases: if some cached cell still has d >= M0 - kDistT, the largest such
+// d is max(d) and that cell a witness.  The targets (all within a few cells
+// of the robot, whose own cell is covered) come from the 5 x 5 tiles around
+// them.  NTH threads; stages the box tiles into ft (kFastTiles words),
+// leaves the cells' new d in cdv, the targets' d in s_d (-1 stays: none),
+// the best (d << 16 | index) in *fkey and a target the 40 x 40 block cannot
+// settle in *ffail; `tried` = false when the box is too large to stage.
+// Ends with a barrier.
+template <int NTH>
+__device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px, int py, const uint64_t* free_t,
+                                          int ccnt, int bx0, int by0, int bx1, int by1, uint64_t* ft,
+                                          const int32_t* cc, const int32_t* cd, uint16_t* cdv, int* s_d,
+                                          uint32_t* fkey, int* ffail, bool& tried) {
+  const int tid = threadIdx.x, E = s.E;
+  const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
+  const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
+  const int nt = nbr * nbc;
+  // the 5 x 5 tiles around the targets' bounding box (the end cells at the
+  // quirk index sit pad cells up-left of the robot, the crop around it)
+  const int tx_c = (min(px - pad - 1, px - s.ego) + max(px - pad + 1, px + s.ego)) >> 1;
+  const int ty_c = (min(py - pad - 1, py - s.ego) + max(py - pad + 1, py + s.ego)) >> 1;
+  const int rti0 = (tx_c >> 3) - 2, rtj0 = (ty_c >> 3) - 2;
+  tried = nt + 25 <= kFastTiles;
+  if (!tried) return;
+  for (int i = tid; i < nt + 25; i += NTH) {
+    int ti, tj;
+    if (i < nt) {
+      const int r = i / nbc;
+      ti = ti0 + r;
+      tj = tj0 + (i - r * nbc);
+    } else {
+      const int r = (i - nt) / 5;
+      ti = rti0 + r;
+      tj = rtj0 + (i - nt - 5 * r);
+    }
+    uint64_t t = (ti >= 0 && ti < s.TR && tj >= 0 && tj < s.TC) ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
+    const int rows = s.Wp - 8 * ti;  // the transform reads map rows < Wp only
+    if (rows < 8) t &= rows > 0 ? low_mask(8 * rows) : 0ull;
+    ft[i] = t;
+  }
+  __syncthreads();
+  uint32_t mykey = 0;
+  for (int k = tid; k < ccnt; k += NTH) {
+    const int32_t cw = cc[k];
+    const int cx = witness_x(cw), cy = witness_y(cw);
+    int d = cd[k];
+    // only box tiles inside the cell's L1 ball of radius d can lower it (a
+    // cell at least d from the box keeps its d): tile rows outward from the
+    // cell's, each row's columns limited by the radius left (d shrinks as
+    // covered cells turn up)
+    const int bdist = max(0, max(bx0 - cx, cx - bx1)) + max(0, max(by0 - cy, cy - by1));
+    if (bdist < d && nt > 0) {
+      const int ct = min(max(cx >> 3, ti0), ti1);  // the box tile row nearest the cell
+      for (int dr = 0; dr <= nbr; ++dr) {
+        bool any = false;
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          const int ti = sg ? ct + dr : ct - dr;
+          if ((sg && dr == 0) || ti < ti0 || ti > ti1) continue;
+          const int dx = max(0, max(8 * ti - cx, cx - (8 * ti + 7)));  // to the tile row band
+          if (dx >= d) continue;
+          any = true;
+          const int rem = d - dx;
+          const int c0 = max(tj0, (cy - rem) >> 3), c1 = min(tj1, (cy + rem) >> 3);
+          const uint64_t* row = ft + (ti - ti0) * nbc - tj0;
+          for (int tj = c0; tj <= c1; ++tj) d = tile_min_dist(row[tj], 8 * ti, 8 * tj, cx, cy, d);
+        }
+        if (!any && dr > 0) {  // both rows at this distance are out of the ball (or the box)
+          const int dlo = 8 * (ct - dr) + 7 < cx ? cx - (8 * (ct - dr) + 7) : 0;
+          const int dhi = 8 * (ct + dr) > cx ? 8 * (ct + dr) - cx : 0;
+          if ((ct - dr < ti0 || dlo >= d) && (ct + dr > ti1 || dhi >= d)) break;
+        }
+      }
+    }
+    cdv[k] = d;
+    mykey = max(mykey, ((uint32_t)d << 16) | (uint32_t)k);
+  }
+  mykey = wave_max_u32(mykey);
+  if ((tid & 63) == 0) atomicMax(fkey, mykey);
+  for (int t = tid; t < T; t += NTH) {
+    // target t, map coordinates: [0, 5) the end cells of the next step at the
+    // quirk index (padded-grid x, y, no pad offset), then the crop
+    int tx, ty;
+    if (t >= 5) {
+      const int r = (t - 5) / E;
+      tx = px - s.ego + r;
+      ty = py - s.ego + (t - 5 - r * E);
+    } else {
+      tx = px + (t == 1 ? 1 : (t == 3 ? -1 : 0)) - pad;
+      ty = py + (t == 2 ? 1 : (t == 4 ? -1 : 0)) - pad;
+    }
+    int d = kInf;
+    for (int i = 0; i < 25; ++i) {
+      const int r = i / 5;
+      d = tile_min_dist(ft[nt + i], 8 * (rti0 + r), 8 * (rtj0 + i - 5 * r), tx, ty, d);
+    }
+    s_d[t] = d;
+    // exact only if no cell outside the 40 x 40 block can be nearer
+    const int b = min(min(tx - 8 * rti0, 8 * rti0 + 39 - tx), min(ty - 8 * rtj0, 8 * rtj0 + 39 - ty)) + 1;
+    if (d > b) *ffail = 1;
+  }
+  __syncthreads();
+}
+
+// a map the cache served: (M, witness), the cached d (exact again: an empty
+// box), the PRE data and the obs crop.  NTH threads.
+template <int NTH>
+__device__ __forceinline__ void cache_serve(const State& s, int T, uint32_t ea, uint32_t fkey, int ccnt, int cM0,
+                                            const uint16_t* cdv, const int* s_d, float* pre_out, float* dist_obs,
+                                            uint32_t* count) {
+  const int tid = threadIdx.x, E = s.E;
+  const int M = (int)(fkey >> 16), kb = (int)(fkey & 0xFFFFu);
+  const float Mf = (float)M;
+  if (tid == 0) {
+    if (count) atomicAdd(count + 3, 1u);  // maps the cache served (MC_FIELD_DIST_CACHED)
+    reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, s.dist_cc[(size_t)ea * kDistK + kb]);
+    reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(ccnt, cM0, 1 << 28, 1 << 28);
+    reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
+  }
+  for (int k = tid; k < ccnt; k += NTH) s.dist_cd[(size_t)ea * kDistK + k] = cdv[k];
+  float* dst = dist_obs + (size_t)ea * E * E;
+  for (int t = 5 + tid; t < T; t += NTH) dst[t - 5] = dist_value((float)s_d[t], Mf);
+  float* pd = pre_out + (size_t)ea * 8;
+  if (tid == 0) pd[0] = Mf;
+  if (tid < 5) pd[1 + tid] = (float)s_d[tid];
+}
+
+// Launch modes of dist_kernel_t:
+//   0  every map (list == nullptr), or the listed maps, each whole in one
+//      workgroup: the cache fast path, else the full transform
+//   (1  the listed maps' cache fast path alone: dist_fast_kernel; a map it
+//      cannot serve goes to the full list, `full`: [0] count, [2] the last
+//      step's count; from [8] (map, theta0) pairs)
+//   2  the full list, each map's strips split over S workgroups ("parts",
+//      S from the list length: the few full transforms of a steady state
+//      step are latency-bound in one workgroup): a part transforms its
+//      strips and publishes its best key, strip maxima, target cells and
+//      cache candidates (State::dist_g*); the last part to finish merges
+//      them and finalises the map as mode 0 does
+constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
+constexpr int kMaxParts = 8;
+constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
+
 template <int kCL>
 __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
                                                             float* __restrict__ pre_out,
                                                             float* __restrict__ dist_obs,
                                                             const uint32_t* __restrict__ list,
-                                                            uint32_t* __restrict__ count) {
+                                                            uint32_t* __restrict__ count, int mode,
+                                                            uint32_t* __restrict__ full) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_cov;
   __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
@@ -190,6 +379,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   __shared__ int s_ffail;
   __shared__ int s_ccount;
   __shared__ int s_kept;
+  __shared__ int s_last;     // mode 2: this part finalises the map
+  __shared__ uint32_t s_base;
   __shared__ int s_smax[kMaxTrack];
   __shared__ int32_t s_ccell[kDistK];
   __shared__ uint16_t s_cdv[kDistK];  // d < 0xFFFF (the transform saturates there)
@@ -206,9 +397,28 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // every map (list == nullptr: one workgroup per (env, agent)), or the maps
   // of a device work list (a fixed grid strides over *count entries: the
   // count is uniform, so every wave reaches the end)
-  const uint32_t n_items = list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x;
-  for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
-    const uint32_t ea = list ? list[it] : it;
+  const int nstrips_all = (RY + kStrip - 1) / kStrip;
+  const uint32_t nF = mode == 2 ? __atomic_load_n(full, __ATOMIC_RELAXED) : 0u;
+  const int S = mode == 2 && nF > 0 ? max(1, min(min(nstrips_all, kMaxParts), (int)(kSplitSlots / nF))) : 1;
+  const uint32_t n_items = mode == 2 ? nF * (uint32_t)S
+                                     : (list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x);
+  const bool strided = mode == 2 || list != nullptr;
+  if (mode == 2 && blockIdx.x == 0 && tid == 0) {
+    // mode 1 has drained the list: its counters for the diagnostics
+    // (MC_FIELD_DIST_LISTED / _CACHED) and empty for the next step's env
+    // kernel (no per-workgroup done counters in modes 1 / 2; the env kernel
+    // empties the full list)
+    count[2] = count[0];
+    count[4] = count[3];
+    count[0] = 0;
+    count[3] = 0;
+  }
+  for (uint32_t it = blockIdx.x; it < n_items; it += (strided ? gridDim.x : n_items)) {
+    const uint32_t fi = mode == 2 ? it / (uint32_t)S : 0u;  // mode 2: full-list entry and part
+    const int part = mode == 2 ? (int)(it - fi * (uint32_t)S) : 0;
+    const uint32_t ea = mode == 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
+    // the strips this workgroup transforms
+    const int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0;
     DSTAMP(ts0);
     const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
@@ -250,76 +460,20 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       bx1 = h1.x;
       by1 = h1.y;
     }
-    // ---- fast path for a listed map with a cache: the cells covered since
-    // the cached d were exact all lie in the box, so the current d of a cached
-    // cell is min(its d, the distance to the box's covered cells).  Every
-    // other cell had d < M0 - kDistT when the cache was taken, and d only
-    // decreases: if some cached cell still has d >= M0 - kDistT, the largest
-    // such d is max(d) and that cell a witness.  The targets (all within a
-    // few cells of the robot, whose own cell is covered) come from the tiles
-    // around the robot.
+    // ---- the top-cell cache fast path (cache_try) for a listed map
     bool fast = false;
-    if (list != nullptr && ccnt > 0) {
-      const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
-      const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
-      const int nt = nbr * nbc;
-      const int rti0 = (px >> 3) - 2, rtj0 = (py >> 3) - 2;  // 5 x 5 tiles around the robot
-      if (nt + 25 <= kFastTiles) {
-        uint64_t* ft = reinterpret_cast<uint64_t*>(G);
-        for (int i = tid; i < nt + 25; i += kDtThreads) {
-          int ti, tj;
-          if (i < nt) {
-            const int r = i / nbc;
-            ti = ti0 + r;
-            tj = tj0 + (i - r * nbc);
-          } else {
-            const int r = (i - nt) / 5;
-            ti = rti0 + r;
-            tj = rtj0 + (i - nt - 5 * r);
-          }
-          uint64_t t = (ti >= 0 && ti < s.TR && tj >= 0 && tj < s.TC) ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
-          const int rows = s.Wp - 8 * ti;  // the transform reads map rows < Wp only
-          if (rows < 8) t &= rows > 0 ? low_mask(8 * rows) : 0ull;
-          ft[i] = t;
-        }
-        __syncthreads();
-        uint32_t mykey = 0;
-        for (int k = tid; k < ccnt; k += kDtThreads) {
-          const int32_t cw = s.dist_cc[(size_t)ea * kDistK + k];
-          const int cx = witness_x(cw), cy = witness_y(cw);
-          int d = s.dist_cd[(size_t)ea * kDistK + k];
-          // every newly covered cell lies in the box: a cell at least d from
-          // the box keeps its d (the cached cells are the map's farthest from
-          // coverage, mostly far from the recent path)
-          const int bdist = max(0, max(bx0 - cx, cx - bx1)) + max(0, max(by0 - cy, cy - by1));
-          for (int i = 0; i < (bdist < d ? nt : 0); ++i) {
-            const int r = i / nbc;
-            d = tile_min_dist(ft[i], 8 * (ti0 + r), 8 * (tj0 + i - r * nbc), cx, cy, d);
-          }
-          s_cdv[k] = d;
-          mykey = max(mykey, ((uint32_t)d << 16) | (uint32_t)k);
-        }
-        mykey = wave_max_u32(mykey);
-        if ((tid & 63) == 0) atomicMax(&s_fkey, mykey);
-        for (int t = tid; t < T; t += kDtThreads) {
-          int tu, tv;
-          target(t, tu, tv);
-          const int tx = tu - pad, ty = tv - pad;  // map coordinates
-          int d = kInf;
-          for (int i = 0; i < 25; ++i) {
-            const int r = i / 5;
-            d = tile_min_dist(ft[nt + i], 8 * (rti0 + r), 8 * (rtj0 + i - 5 * r), tx, ty, d);
-          }
-          s_d[t] = d;
-          // exact only if no cell outside the 40 x 40 block can be nearer
-          const int b = min(min(tx - 8 * rti0, 8 * rti0 + 39 - tx), min(ty - 8 * rtj0, 8 * rtj0 + 39 - ty)) + 1;
-          if (d > b) s_ffail = 1;
-        }
-        __syncthreads();
-        fast = s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
-      }
+    if (mode != 2 && list != nullptr && ccnt > 0) {
+      bool tried = false;
+      cache_try<kDtThreads>(s, pad, T, px, py, free_t, ccnt, bx0, by0, bx1, by1, reinterpret_cast<uint64_t*>(G),
+                            s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, s_cdv, s_d, &s_fkey,
+                            &s_ffail, tried);
+      fast = tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
     }
-    const int nstrips_all = (RY + kStrip - 1) / kStrip;
+    uint64_t tsf = 0;
+    DSTAMP(tsf);
+    // the exact current d of the cached cells (the fast path computed them
+    // before it failed): a lower bound of the new max(d)
+    const int theta0 = mode == 2 ? (int)full[9 + 2 * fi] : ((s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0);
     if (!fast) {
       for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
       {
@@ -331,15 +485,26 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         uint8_t* crow = reinterpret_cast<uint8_t*>(G);
         const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
         const int RB = RWm * 8;           // bytes per map row
-#pragma unroll 4
-        for (int i = tid; i < s.MT; i += kDtThreads) {
-          const uint64_t t = free_t[i];
-          const int blk = i >> 4, bi = blk / s.TCS, bj = blk - bi * s.TCS;
-          const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
-          if (ti < s.TR && tj < s.TC) {
+        // eight tiles' loads in flight per thread, then their bytes; the
+        // block row of tile i by a magic reciprocal (no division)
+        const uint32_t mT = magic_div((uint32_t)s.TCS);
+        for (int i0 = tid; i0 < s.MT; i0 += 8 * kDtThreads) {
+          uint64_t tv[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r)
-              if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(t >> (8 * r));
+          for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kDtThreads;
+            tv[k] = i < s.MT ? free_t[i] : 0ull;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kDtThreads;
+            const int blk = i >> 4, bi = mT ? (int)__umulhi((uint32_t)blk, mT) : blk, bj = blk - bi * s.TCS;
+            const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
+            if (i < s.MT && ti < s.TR && tj < s.TC) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r)
+                if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(tv[k] >> (8 * r));
+            }
           }
         }
         for (int X = tid; X < s.Wp; X += kDtThreads)
@@ -347,18 +512,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         __syncthreads();
         const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
         int any = 0;
-        for (int i = tid; i < RX * RW; i += kDtThreads) {
-          const int u = i / RW, w = i - u * RW, X = u - pad;
-          uint64_t c = 0;
-          if (X >= 0 && X < s.Wp) {  // map columns [64 w - pad, 64 w - pad + 64)
-            const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
-            const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
-            const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
-            c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
+        for (int u = tid; u < RX; u += kDtThreads) {  // a row per thread
+          const int X = u - pad;
+          const bool in = X >= 0 && X < s.Wp;
+          for (int w = 0; w < RW; ++w) {
+            uint64_t c = 0;
+            if (in) {  // map columns [64 w - pad, 64 w - pad + 64)
+              const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
+              const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
+              const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
+              c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
+            }
+            c &= (w == RW - 1) ? last : ~0ull;
+            Cb[u * RW + w] = c;
+            any |= c != 0;
           }
-          c &= (w == RW - 1) ? last : ~0ull;
-          Cb[i] = c;
-          any |= c != 0;
         }
         if (any) s_cov = 1;
       }
@@ -474,7 +642,14 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       __syncthreads();  // every G read of the strip is done: the next row pass may write
       // minima over the pair's chunks before / after this one (its 32 chunks
       // are the lanes of one half wave)
-      u16x2 run = excl_prefix_min32(pm), sfx = excl_suffix_min32(sm);
+      u16x2 run, sfx;
+      if constexpr (kCh == 64) {
+        run = excl_prefix_min64(pm);
+        sfx = excl_suffix_min64(sm);
+      } else {
+        run = excl_prefix_min32(pm);
+        sfx = excl_suffix_min32(sm);
+      }
       // suffix scan: the "down" distance min_{u'>=u} g(u') + u' - u
 #pragma unroll
       for (int i = kCL - 1; i >= 0; --i) {
@@ -549,20 +724,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       }
     };
     const int nstrips = (cov && !fast) ? nstrips_all : 0;
-    // the cache's cells in the same pass: every cell with d >= M - kDistT
+    // The cache's cells in the same pass: every cell with d >= M - kDistT
     // (M = the new max, known only at the end) has d >= any lower bound of
-    // M, less kDistT.  Bounds: the exact current d of the cached cells (the
-    // fast path computed them before it failed) and the strips' maxima so far
-    // (s_smax two strips back: past two barriers).  The list then holds a
-    // superset, filtered at the end; without a bound (no cache tried) or on
-    // overflow, a second pass over the strips collects them.
-    const int theta0 = (s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0;
-    // Strip pruning (with that bound): a strip whose max(d) at the last full
-    // transform (State::dist_sm, an upper bound now: d only decreases) is
-    // below theta0 - kDistT holds neither the new max, nor a witness, nor a
-    // cache cell; only its rows' last covered column is carried.  The
-    // strips of the target cells always run.
-    // Strip pruning (with that bound): a strip whose max(d) at the last full
+    // M, less kDistT.  Bounds: theta0 and the strips' maxima so far (s_smax
+    // two strips back: past two barriers).  The list then holds a superset,
+    // filtered at the end; without a bound (no cache tried) or on overflow, a
+    // second pass over the strips collects them.
+    // Strip pruning (with theta0): a strip whose max(d) at the last full
     // transform (State::dist_sm, an upper bound now: d only decreases) is
     // below theta0 - kDistT holds neither the new max, nor a witness, nor a
     // cache cell; only its rows' last covered column is carried.  The
@@ -573,8 +741,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     const uint16_t* smb = s.dist_ch ? s.dist_sm + (size_t)ea * kMaxTrack : nullptr;
     int runmax = 0;
     uint64_t ran = 0;  // strips transformed (their s_smax are exact maxima)
-    for (int st = 0; st < nstrips; ++st) {
-      if (st >= 2 && st - 2 < kMaxTrack && ((ran >> (st - 2)) & 1ull)) runmax = max(runmax, s_smax[st - 2]);
+    const int s_from = nstrips > 0 ? st_lo : 0, s_to = nstrips > 0 ? st_hi : 0;
+    if (s_from > 0 && s_from < s_to) {  // a part's first strip: each row's last covered column left of it
+      const int c0 = s_from * kStrip, w = c0 >> 6;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int u = tid + q * kDtThreads;
+        if (u >= RX) continue;
+        uint64_t m = (c0 & 63) ? Cb[u * RW + w] & low_mask(c0 & 63) : 0ull;
+        int k = w;
+        while (!m && k > 0) m = Cb[u * RW + --k];
+        if (m) lastL[q] = 64 * k + 63 - __clzll((unsigned long long)m);
+      }
+    }
+    for (int st = s_from; st < s_to; ++st) {
+      if (st - 2 >= s_from && st - 2 < kMaxTrack && ((ran >> (st - 2)) & 1ull)) runmax = max(runmax, s_smax[st - 2]);
       if (prune) {
         const int c0 = st * kStrip, bound = smb[st];
         if (bound < theta0 - kDistT && !(c0 + kStrip > tv_lo && c0 <= tv_hi)) {
@@ -606,20 +787,76 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                             ((unsigned long long)ubest << 16) | (unsigned long long)vbest);
     }
     __syncthreads();
+    if (mode == 2 && S > 1 && !fast) {
+      // ---- a part: publish the best key, the targets it holds (raw d in
+      // the output buffers), its strips' maxima and its cache candidates
+      if (tid == 0 && s_key) atomicMax(s.dist_gkey + ea, s_key);
+      for (int t = tid; t < T; t += kDtThreads)
+        if (s_d[t] >= 0) {
+          if (t < 5) pre_out[(size_t)ea * 8 + 1 + t] = (float)s_d[t];
+          else dist_obs[(size_t)ea * E * E + (t - 5)] = (float)s_d[t];
+        }
+      for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
+        if ((ran >> st) & 1ull) s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
+      if (kOnePass && theta0 > 0) {
+        const int n = s_ccount;
+        if (tid == 0) s_base = atomicAdd(s.dist_gcnt + ea, (uint32_t)(n <= kDistK ? n : kGCand + 1));
+        __syncthreads();
+        const uint32_t base = s_base;
+        if (n <= kDistK)
+          for (int k = tid; k < n; k += kDtThreads)
+            if (base + k < (uint32_t)kGCand) s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
+      }
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) s_last = atomicAdd(s.dist_gdone + ea, 1u) == (uint32_t)(S - 1);
+      __syncthreads();
+      if (!s_last) {
+        __syncthreads();  // the LDS is reused by the next item
+        continue;
+      }
+      // ---- the last part: merge every part's partials into this workgroup's
+      // state, then finalise the map as a whole-map workgroup does
+      __threadfence();
+      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
+      const unsigned long long gk = s.dist_gkey[ea];
+      const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
+      for (int t = tid; t < T; t += kDtThreads)
+        s_d[t] = (int)(t < 5 ? pre_out[(size_t)ea * 8 + 1 + t] : dist_obs[(size_t)ea * E * E + (t - 5)]);
+      for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
+        s_smax[st] = s.dist_sm[(size_t)ea * kMaxTrack + st];
+      __syncthreads();  // every part's own s_key / s_ccount reads are done
+      if (tid == 0) {
+        s_key = gk;
+        s_ccount = 0;
+      }
+      __syncthreads();
+      if (total <= (uint32_t)kGCand)
+        for (int k = tid; k < (int)total; k += kDtThreads) {
+          const int2 c = s.dist_gcand[(size_t)ea * kGCand + k];
+          if (c.y >= thr) {
+            const int j = atomicAdd(&s_ccount, 1);
+            if (j < kDistK) {
+              s_ccell[j] = c.x;
+              s_cdv[j] = (uint16_t)c.y;
+            }
+          }
+        }
+      __syncthreads();
+      if (tid == 0) {
+        if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
+        s.dist_gkey[ea] = 0;  // zero for the map's next split transform
+        s.dist_gdone[ea] = 0;
+        s.dist_gcnt[ea] = 0;
+      }
+      __syncthreads();
+    }
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
     const int M = fast ? (int)(s_fkey >> 16) : (cov ? (int)(s_key >> 48) : -1);
     const float Mf = (float)M;
     if (fast) {
-      const int kb = (int)(s_fkey & 0xFFFFu);
-      if (tid == 0) {
-        atomicAdd(count + 3, 1u);  // maps the cache served (MC_FIELD_DIST_CACHED)
-        reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, s.dist_cc[(size_t)ea * kDistK + kb]);
-        // the cached d are exact again: an empty box
-        reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(ccnt, cM0, 1 << 28, 1 << 28);
-        reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
-      }
-      for (int k = tid; k < ccnt; k += kDtThreads) s.dist_cd[(size_t)ea * kDistK + k] = s_cdv[k];
+      cache_serve<kDtThreads>(s, T, ea, s_fkey, ccnt, cM0, s_cdv, s_d, pre_out, dist_obs, count);
     } else {
       if (tid == 0) {  // M unknown (-1) while nothing is covered: every step recomputes it
         const int wu = (int)((s_key >> 16) & 0xFFFF), wv = (int)(s_key & 0xFFFF);
@@ -681,14 +918,16 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       }
     }
-    if (post) {
-      float* dst = dist_obs + (size_t)ea * E * E;
-      for (int t = 5 + tid; t < T; t += kDtThreads)
-        dst[t - 5] = dist_value((float)(cov ? s_d[t] : -1), Mf);
+    if (!fast) {
+      if (post) {
+        float* dst = dist_obs + (size_t)ea * E * E;
+        for (int t = 5 + tid; t < T; t += kDtThreads)
+          dst[t - 5] = dist_value((float)(cov ? s_d[t] : -1), Mf);
+      }
+      float* pd = pre_out + (size_t)ea * 8;
+      if (tid == 0) pd[0] = Mf;
+      if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
     }
-    float* pd = pre_out + (size_t)ea * 8;
-    if (tid == 0) pd[0] = Mf;
-    if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
     DSTAMP(ts3);
 #ifdef MC_DIST_STAMPS
     if (tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u) {
@@ -696,11 +935,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         const uint64_t d = (b - a) >> 4;
         return d < 0xFFFFull ? d : 0xFFFFull;
       };
+      const uint64_t ff = min((tsf - ts0) >> 6, (uint64_t)0x1FFF);  // the fast-path attempt, cycles/64
       s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, ts3) << 32) | dflags |
-                     (fast ? 1ull << 48 : 0ull);
+                     (fast ? 1ull << 48 : 0ull) | (ff << 51);
     }
 #else
-    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)dflags;
+    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)tsf; (void)dflags;
 #endif
     __syncthreads();  // the LDS is reused by the next item
   }
@@ -736,9 +976,91 @@ size_t dist_static_lds_bytes() {
   return (size_t)kDistK * (sizeof(int32_t) + sizeof(uint16_t)) + kMaxTrack * sizeof(int) + 64;
 }
 
+// Mode 1 of the listed maps: the cache fast path alone, in small workgroups
+// with a small LDS (every listed map of a step resident at once: the
+// transform kernel's LDS admits two workgroups per CU); a map it cannot
+// serve goes to the full list with its theta0 (the exact max of its cached
+// cells' d, a lower bound of the new max(d); 0 without a try).
+constexpr int kFastThreads = 256;
+constexpr int kFastBuf = 128;  // full-list entries a workgroup buffers before one atomic
+
+__global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pad, float* __restrict__ pre_out,
+                                                                 float* __restrict__ dist_obs,
+                                                                 const uint32_t* __restrict__ list,
+                                                                 uint32_t* __restrict__ count,
+                                                                 uint32_t* __restrict__ full) {
+  extern __shared__ __attribute__((aligned(16))) int s_dyn[];  // the targets' d: [5 + E*E]
+  __shared__ uint64_t ft[kFastTiles];
+  __shared__ uint16_t cdv[kDistK];
+  __shared__ uint32_t s_fkey;
+  __shared__ int s_ffail;
+  __shared__ uint32_t s_served, s_nf, s_fbase, s_nc;
+  __shared__ uint2 s_fl[kFastBuf];     // this workgroup's maps for the full list
+  __shared__ uint32_t s_cl[kFastBuf];  // this chunk's maps with a cache
+  const int tid = threadIdx.x;
+  const int T = 5 + s.E * s.E;
+  const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
+  if (tid == 0) s_served = s_nf = 0;
+  // a contiguous share of the list per workgroup, kFastBuf maps at a time:
+  // one thread per map reads its cache header (a map without a cache goes
+  // straight to the full list), then the workgroup tries the cache of each
+  // map that has one
+  auto to_full = [&](uint32_t ea, uint32_t theta) {  // (one thread)
+    const uint32_t k = atomicAdd(&s_nf, 1u);
+    if (k < (uint32_t)kFastBuf) s_fl[k] = make_uint2(ea, theta);
+    else reinterpret_cast<uint2*>(full + 8)[atomicAdd(full, 1u)] = make_uint2(ea, theta);
+  };
+  const uint32_t per = (n_items + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = min(n_items, blockIdx.x * per), hi = min(n_items, lo + per);
+  for (uint32_t c0 = lo; c0 < hi; c0 += kFastBuf) {
+    const uint32_t c1 = min(hi, c0 + (uint32_t)kFastBuf);
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    for (uint32_t i = c0 + tid; i < c1; i += kFastThreads) {
+      const uint32_t ea = list[i];
+      if (s.dist_ch[(size_t)ea * 8] > 0) s_cl[atomicAdd(&s_nc, 1u)] = ea;
+      else to_full(ea, 0u);
+    }
+    __syncthreads();
+    const uint32_t nc = s_nc;
+    for (uint32_t j = 0; j < nc; ++j) {
+      const uint32_t ea = s_cl[j];
+      const int4 h0 = reinterpret_cast<const int4*>(s.dist_ch + (size_t)ea * 8)[0];
+      const int2 h1 = reinterpret_cast<const int2*>(s.dist_ch + (size_t)ea * 8)[2];
+      const int ccnt = h0.x, cM0 = h0.y;
+      const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
+      for (int t = tid; t < T; t += kFastThreads) s_dyn[t] = -1;
+      if (tid == 0) {
+        s_fkey = 0;
+        s_ffail = 0;
+      }
+      __syncthreads();
+      bool tried = false;
+      cache_try<kFastThreads>(s, pad, T, pp.x, pp.y, s.freem + (size_t)ea * s.MT, ccnt, h0.z, h0.w, h1.x, h1.y, ft,
+                              s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, cdv, s_dyn, &s_fkey,
+                              &s_ffail, tried);
+      if (tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT) {
+        cache_serve<kFastThreads>(s, T, ea, s_fkey, ccnt, cM0, cdv, s_dyn, pre_out, dist_obs, nullptr);
+        if (tid == 0) ++s_served;
+      } else if (tid == 0) {
+        to_full(ea, tried ? (s_fkey >> 16) : 0u);
+      }
+      __syncthreads();  // the LDS is reused by the next map
+    }
+  }
+  if (tid == 0 && s_nf > (uint32_t)kFastBuf) s_nf = kFastBuf;  // the rest went to the list directly
+  // one atomic per workgroup for the served count and for the full list
+  if (tid == 0) {
+    if (s_served) atomicAdd(count + 3, s_served);  // MC_FIELD_DIST_CACHED
+    s_fbase = s_nf ? atomicAdd(full, s_nf) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < s_nf; k += kFastThreads) reinterpret_cast<uint2*>(full + 8)[s_fbase + k] = s_fl[k];
+}
+
 // the instantiation whose register chunk holds ceil(RX / kChunks) rows
 static hipError_t launch_full(const State& s, int pad, int post, float* pre_out, float* dist_obs,
-                              const uint32_t* list, uint32_t* count, unsigned grid,
+                              const uint32_t* list, uint32_t* count, unsigned grid, int mode, uint32_t* full,
                               hipStream_t stream) {
   const int RX = s.Wp + 2 * pad, cl = chunk_rows(RX);
   const size_t lds = dist_lds_bytes(s, pad);
@@ -750,19 +1072,25 @@ static hipError_t launch_full(const State& s, int pad, int post, float* pre_out,
       if (e_ != hipSuccess) return e_;                                                         \
     }                                                                                          \
     hipLaunchKernelGGL(dist_kernel_t<CL>, dim3(grid), dim3(kDtThreads), lds, stream, s, pad,   \
-                       post, pre_out, dist_obs, list, count);                                  \
+                       post, pre_out, dist_obs, list, count, mode, full);                      \
   } while (0)
-  if (cl == 8) MC_DT(8);
-  else if (cl == 17) MC_DT(17);
-  else MC_DT(26);  // kMaxRows / kCh
+  if constexpr (kCh == 64) {
+    if (cl == 4) MC_DT(4);
+    else if (cl == 9) MC_DT(9);
+    else MC_DT(13);  // kMaxRows / kCh
+  } else {
+    if (cl == 8) MC_DT(8);
+    else if (cl == 17) MC_DT(17);
+    else MC_DT(26);  // kMaxRows / kCh
+  }
 #undef MC_DT
   return hipGetLastError();
 }
 
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream) {
-  return launch_full(s, pad, post, pre_out, dist_obs, nullptr, nullptr,
-                     (unsigned)((size_t)s.B * s.N), stream);
+  return launch_full(s, pad, post, pre_out, dist_obs, nullptr, nullptr, (unsigned)((size_t)s.B * s.N), 0,
+                     nullptr, stream);
 }
 
 // --------------------------------------------------------------------------
@@ -773,14 +1101,22 @@ hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float*
 // targets (the E x E crop and the 5 end cells of the next step) are near the
 // robot, so the env kernel settles their d from the agent's staged block
 // (mc_env_kernel.hip dist_window) and lists only the maps with an unknown M
-// or a target the block cannot settle; the full transform runs over that
-// list.  The list grid is fixed (hipGraph capture) and strides.
+// or a target the block cannot settle.  With the top-cell cache, the listed
+// maps first try the cache (mode 1) and the rest run split over workgroups
+// (mode 2; `full`: the full list); without it, each listed map runs whole
+// (mode 0).  The grids are fixed (hipGraph capture) and stride.
 // --------------------------------------------------------------------------
 hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* dist_obs,
-                              uint32_t* list, uint32_t* count, hipStream_t stream) {
+                              uint32_t* list, uint32_t* count, uint32_t* full, hipStream_t stream) {
   const size_t maps = (size_t)s.B * s.N;
   const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
-  return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, stream);
+  if (!full || !s.dist_ch)
+    return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, 0, nullptr, stream);
+  hipLaunchKernelGGL(dist_fast_kernel, dim3(grid), dim3(kFastThreads), (size_t)(5 + s.E * s.E) * 4, stream, s, pad,
+                     pre_out, dist_obs, list, count, full);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, 2048, 2, full, stream);
 }
 
 }  // namespace mc

@@ -1928,9 +1928,22 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       }
     }
   }
-  if (valid && dlist) {  // the full transform's work list (mc_dist.hip launch_dist_listed)
-    const uint32_t slot = atomicAdd(s.dist_cnt, 1u);
-    s.dist_cnt[5 + slot] = (uint32_t)e * (uint32_t)N + (uint32_t)C.sub;
+  if (s.dist) {
+    // the full transform's work list (mc_dist.hip launch_dist_listed): one
+    // atomic per wave, the wave's entries at consecutive slots
+    const bool me = valid && dlist;
+    const uint64_t m = __ballot(me);
+    if (m) {
+      const int lane = (int)(threadIdx.x & 63), leader = __ffsll((unsigned long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(s.dist_cnt, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, leader);
+      if (me) s.dist_cnt[5 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)e * (uint32_t)N + (uint32_t)C.sub;
+    }
+    if (s.dist_full && blockIdx.x == 0 && threadIdx.x == 0) {  // the last step's full list is done
+      s.dist_full[2] = s.dist_full[0];
+      s.dist_full[0] = 0;
+    }
   }
   STAMP(8);
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&

@@ -122,6 +122,10 @@ struct State {
   // mc_dist.hip dist_kernel_t)
   float* dist_obs_out;
   uint32_t* dist_cnt;
+  // the split transform's full list (mc_dist.hip modes 1 / 2; null without
+  // it): the env kernel empties it for the step (its count read by the last
+  // step's mode 2 is done by then)
+  uint32_t* dist_full;
   // dist_reward top-cell cache (mc_dist.hip; null when off, e.g. with map
   // sharing): per map kDistK cells (witness packing) and their d, and a
   // header [8]: count (-1: none), M0 (max(d) when the cells were taken),
@@ -136,6 +140,13 @@ struct State {
   // strip of the extended grid ([B][N][kDistStrips] u16: the strip maxima of
   // the last full transform; d only decreases), valid while the cache is
   uint16_t* dist_sm;
+  // with the cache: the split full transform's per-map partials (mc_dist.hip
+  // mode 2; zero between uses): the best key, the parts done, the candidate
+  // cells published and the candidates [B][N][kDistK] (cell, d)
+  unsigned long long* dist_gkey;
+  uint32_t* dist_gdone;
+  uint32_t* dist_gcnt;
+  int2* dist_gcand;
   // episode record, written when an env reports done (before an auto-reset
   // clears the counters): percent_covered() and _currstep at the end
   double* ep_pc;

@@ -58,6 +58,7 @@ def main():
     kept = (s >> np.uint64(49)) & np.uint64(1)
     second = (s >> np.uint64(50)) & np.uint64(1)
     ph = [((s >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
+    ph.insert(0, (s >> np.uint64(51)).astype(np.int64) * 64)  # the fast-path attempt (part of stage)
     for name, m in (("fast path", fast == 1), ("full, one-pass list", (fast == 0) & (kept == 1)),
                     ("full, second pass", (fast == 0) & (second == 1)),
                     ("full, no cache", (fast == 0) & (kept == 0) & (second == 0))):
@@ -65,7 +66,7 @@ def main():
             print(f"  {name:22s} n=0")
             continue
         row = "  ".join(f"{lab} med {np.median(p[m]):8.0f} p90 {np.percentile(p[m], 90):8.0f} max {p[m].max():8d}"
-                        for lab, p in zip(("stage", "strips", "cache"), ph))
+                        for lab, p in zip(("fast try", "stage", "strips", "cache"), ph))
         print(f"  {name:22s} n={m.sum():5d}  {row}")
 
 

@@ -14,14 +14,19 @@ for spec in ${VARIANTS}; do
   rc=$?; echo "== $spec rc=$rc"; [ $rc -ne 0 ] && exit $rc
   python3 - "$OUT/$name/run_kernel_trace.csv" "$K" <<'PY'
 import csv, statistics, sys, collections
-K = int(sys.argv[2]); d = collections.defaultdict(list)
-for r in csv.DictReader(open(sys.argv[1])):
-    d[r["Kernel_Name"].split("(")[0][:70]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-tot = 0
+K = int(sys.argv[2])
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+rows = [r for r in rows if "rocclr" not in r["Kernel_Name"] and "random_actions" not in r["Kernel_Name"]
+        and "at::" not in r["Kernel_Name"]]
+env = [i for i, r in enumerate(rows) if "env_kernel" in r["Kernel_Name"]]
+first = env[-K]  # the timed steps: from the K-th last env kernel on
+d = collections.defaultdict(float)
+for r in rows[first:]:
+    d[r["Kernel_Name"].split("(")[0][:70]] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 for k, v in d.items():
-    if len(v) > K and "rocclr" not in k and "random_actions" not in k:
-        m = statistics.mean(v[-K:]); tot += m; print(f"  {k:70s} {m:9.2f} us")
-print(f"  step total {tot:.2f} us")
+    print(f"  {k:70s} {v / K:9.2f} us per step")
+span = (int(rows[-1]["End_Timestamp"]) - int(rows[first]["Start_Timestamp"])) / 1e3
+print(f"  step total {sum(d.values()) / K:.2f} us (trace span {span / K:.2f} us per step)")
 PY
 done
 exit 0
