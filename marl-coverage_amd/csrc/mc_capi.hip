@@ -411,12 +411,12 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     const char* dc = getenv("MARLCOV_DIST_CACHE");
     if (!c.map_sharing && !(dc && dc[0] == '0')) {
       void *cc = nullptr, *cd = nullptr, *ch = nullptr, *sm = nullptr;
-      void *gk = nullptr, *gd = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr;
+      void *gk = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr;
       const size_t maps = (size_t)s.B * s.N;
       if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
           dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess ||
           dev_alloc(E, &sm, maps * mc::kDistStrips * 2) != MC_OK || dev_alloc(E, &gk, maps * 8) != MC_OK ||
-          dev_alloc(E, &gd, maps * 4) != MC_OK || dev_alloc(E, &gc, maps * 4) != MC_OK ||
+          dev_alloc(E, &gc, maps * 4) != MC_OK ||
           dev_alloc(E, &ga, maps * 4 * mc::kDistK * 8) != MC_OK || dev_alloc(E, &fl, (maps * 2 + 8) * 4) != MC_OK) {
         std::string msg = g_err;
         mc_destroy(E);
@@ -427,7 +427,6 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       E->s.dist_ch = (int32_t*)ch;
       E->s.dist_sm = (uint16_t*)sm;
       E->s.dist_gkey = (unsigned long long*)gk;
-      E->s.dist_gdone = (uint32_t*)gd;
       E->s.dist_gcnt = (uint32_t*)gc;
       E->s.dist_gcand = (int2*)ga;
       // MARLCOV_DIST_SPLIT=0: every listed map's full transform in one workgroup

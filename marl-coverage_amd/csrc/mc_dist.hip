@@ -227,12 +227,15 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
 // leaves the cells' new d in cdv, the targets' d in s_d (-1 stays: none),
 // the best (d << 16 | index) in *fkey and a target the 40 x 40 block cannot
 // settle in *ffail; `tried` = false when the box is too large to stage.
+// `span` (optional, 2 * kSpan words): the staged box's covered extent per
+// row and per column, for the cells outside the box's column or row band.
 // Ends with a barrier.
+constexpr int kSpan = 512;  // box rows / columns the span arrays hold
 template <int NTH>
 __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px, int py, const uint64_t* free_t,
                                           int ccnt, int bx0, int by0, int bx1, int by1, uint64_t* ft,
                                           const int32_t* cc, const int32_t* cd, uint16_t* cdv, int* s_d,
-                                          uint32_t* fkey, int* ffail, bool& tried) {
+                                          uint32_t* fkey, int* ffail, bool& tried, uint32_t* span = nullptr) {
   const int tid = threadIdx.x, E = s.E;
   const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
   const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
@@ -261,6 +264,40 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     ft[i] = t;
   }
   __syncthreads();
+  // the staged box (tile-aligned): rows [X0, X0 + 8 nbr), columns [Y0, Y0 + 8 nbc)
+  const int X0 = 8 * ti0, Y0 = 8 * tj0, NR = 8 * nbr, NC = 8 * nbc;
+  const bool rspan = span && nt > 0 && NR <= kSpan, cspan = span && nt > 0 && NC <= kSpan;
+  if (rspan || cspan) {
+    // row X: the first and last covered column (offsets from Y0; 0xFFFF: none);
+    // column Y: the first and last covered row (offsets from X0)
+    for (int i = tid; i < (rspan ? NR : 0) + (cspan ? NC : 0); i += NTH) {
+      uint32_t lo = 0xFFFFu, hi = 0u;
+      if (rspan && i < NR) {
+        const uint64_t* trow = ft + (i >> 3) * nbc;
+        const int sh = 8 * (i & 7);
+        for (int j = 0; j < nbc; ++j) {
+          const uint32_t b = (uint32_t)(trow[j] >> sh) & 0xFFu;
+          if (b) {
+            if (lo == 0xFFFFu) lo = 8 * j + __ffs(b) - 1;
+            hi = 8 * j + 31 - __clz(b);
+          }
+        }
+        span[i] = lo | (hi << 16);
+      } else {
+        const int y = i - (rspan ? NR : 0);
+        const uint64_t m = 0x0101010101010101ull << (y & 7);
+        for (int r = 0; r < nbr; ++r) {
+          const uint64_t b = ft[r * nbc + (y >> 3)] & m;
+          if (b) {
+            if (lo == 0xFFFFu) lo = 8 * r + (__ffsll((unsigned long long)b) - 1) / 8;
+            hi = 8 * r + (63 - __clzll((unsigned long long)b)) / 8;
+          }
+        }
+        span[kSpan + y] = lo | (hi << 16);
+      }
+    }
+    __syncthreads();
+  }
   uint32_t mykey = 0;
   for (int k = tid; k < ccnt; k += NTH) {
     const int32_t cw = cc[k];
@@ -271,7 +308,34 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     // cell's, each row's columns limited by the radius left (d shrinks as
     // covered cells turn up)
     const int bdist = max(0, max(bx0 - cx, cx - bx1)) + max(0, max(by0 - cy, cy - by1));
-    if (bdist < d && nt > 0) {
+    const int gy = max(Y0 - cy, cy - (Y0 + NC - 1)), gx = max(X0 - cx, cx - (X0 + NR - 1));
+    if (bdist < d && nt > 0 && ((rspan && gy > 0) || (cspan && gx > 0))) {
+      // the cell is beside the box's column band (or row band): in every box
+      // row the nearest covered cell is that row's first (last) covered
+      // column, so d = min over rows |cx - X| + the column gap; rows outward
+      // from the cell's, while the row distance alone stays below d
+      const bool byrow = rspan && gy > 0 && (!(cspan && gx > 0) || NR <= NC);
+      const int a = byrow ? cx - X0 : cy - Y0, n = byrow ? NR : NC;  // the cell along the span axis
+      const int o = byrow ? cy - Y0 : cx - X0;                          // and across it (outside [0, n'))
+      const uint32_t* sp = byrow ? span : span + kSpan;
+      const int ac = min(max(a, 0), n - 1);
+      for (int dr = 0; dr < n; ++dr) {
+        bool live = false;
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          const int q = sg ? ac + dr : ac - dr;
+          if ((sg && dr == 0) || q < 0 || q >= n) continue;
+          const int dq = abs(a - q);
+          if (dq + (byrow ? gy : gx) >= d) continue;
+          live = true;
+          const uint32_t v = sp[q];
+          if ((v & 0xFFFFu) != 0xFFFFu) d = min(d, dq + (o < 0 ? (int)(v & 0xFFFFu) - o : o - (int)(v >> 16)));
+        }
+        // both directions out of the span or the ball: the distance along
+        // the axis only grows from here
+        if (!live) break;
+      }
+    } else if (bdist < d && nt > 0) {
       const int ct = min(max(cx >> 3, ti0), ti1);  // the box tile row nearest the cell
       for (int dr = 0; dr <= nbr; ++dr) {
         bool any = false;
@@ -312,6 +376,10 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
       ty = py + (t == 2 ? 1 : (t == 4 ? -1 : 0)) - pad;
     }
     int d = kInf;
+    {  // the target's own tile first: a covered target ends the search at once
+      const int r = min(max((tx >> 3) - rti0, 0), 4), c = min(max((ty >> 3) - rtj0, 0), 4);
+      d = tile_min_dist(ft[nt + 5 * r + c], 8 * (rti0 + r), 8 * (rtj0 + c), tx, ty, d);
+    }
     for (int i = 0; i < 25; ++i) {
       const int r = i / 5;
       d = tile_min_dist(ft[nt + i], 8 * (rti0 + r), 8 * (rtj0 + i - 5 * r), tx, ty, d);
@@ -357,8 +425,13 @@ __device__ __forceinline__ void cache_serve(const State& s, int T, uint32_t ea, 
 //      S from the list length: the few full transforms of a steady state
 //      step are latency-bound in one workgroup): a part transforms its
 //      strips and publishes its best key, strip maxima, target cells and
-//      cache candidates (State::dist_g*); the last part to finish merges
-//      them and finalises the map as mode 0 does
+//      cache candidates (State::dist_g*); with S == 1 the one part
+//      finalises the map as mode 0 does
+//   3  the full list after mode 2 (S > 1): one workgroup per map merges the
+//      parts' partials and finalises the map (the bitboard is staged only
+//      for a second cache pass).  A launch boundary orders the parts'
+//      stores before the merge: no per-map done counter, no device-scope
+//      fences between the XCDs' L2s
 constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
 constexpr int kMaxParts = 8;
 constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
@@ -379,7 +452,6 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   __shared__ int s_ffail;
   __shared__ int s_ccount;
   __shared__ int s_kept;
-  __shared__ int s_last;     // mode 2: this part finalises the map
   __shared__ uint32_t s_base;
   __shared__ int s_smax[kMaxTrack];
   __shared__ int32_t s_ccell[kDistK];
@@ -398,11 +470,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // of a device work list (a fixed grid strides over *count entries: the
   // count is uniform, so every wave reaches the end)
   const int nstrips_all = (RY + kStrip - 1) / kStrip;
-  const uint32_t nF = mode == 2 ? __atomic_load_n(full, __ATOMIC_RELAXED) : 0u;
-  const int S = mode == 2 && nF > 0 ? max(1, min(min(nstrips_all, kMaxParts), (int)(kSplitSlots / nF))) : 1;
-  const uint32_t n_items = mode == 2 ? nF * (uint32_t)S
-                                     : (list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x);
-  const bool strided = mode == 2 || list != nullptr;
+  const uint32_t nF = mode >= 2 ? __atomic_load_n(full, __ATOMIC_RELAXED) : 0u;
+  const int S = mode >= 2 && nF > 0 ? max(1, min(min(nstrips_all, kMaxParts), (int)(kSplitSlots / nF))) : 1;
+  const uint32_t n_items = mode == 2   ? nF * (uint32_t)S
+                           : mode == 3 ? (S > 1 ? nF : 0u)
+                                       : (list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x);
+  const bool strided = mode >= 2 || list != nullptr;
   if (mode == 2 && blockIdx.x == 0 && tid == 0) {
     // mode 1 has drained the list: its counters for the diagnostics
     // (MC_FIELD_DIST_LISTED / _CACHED) and empty for the next step's env
@@ -414,9 +487,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     count[3] = 0;
   }
   for (uint32_t it = blockIdx.x; it < n_items; it += (strided ? gridDim.x : n_items)) {
-    const uint32_t fi = mode == 2 ? it / (uint32_t)S : 0u;  // mode 2: full-list entry and part
+    // modes 2 / 3: the full-list entry (and mode 2's part)
+    const uint32_t fi = mode == 2 ? it / (uint32_t)S : (mode == 3 ? it : 0u);
     const int part = mode == 2 ? (int)(it - fi * (uint32_t)S) : 0;
-    const uint32_t ea = mode == 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
+    const uint32_t ea = mode >= 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
     // the strips this workgroup transforms
     const int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0;
@@ -462,7 +536,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     }
     // ---- the top-cell cache fast path (cache_try) for a listed map
     bool fast = false;
-    if (mode != 2 && list != nullptr && ccnt > 0) {
+    if (mode < 2 && list != nullptr && ccnt > 0) {
       bool tried = false;
       cache_try<kDtThreads>(s, pad, T, px, py, free_t, ccnt, bx0, by0, bx1, by1, reinterpret_cast<uint64_t*>(G),
                             s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, s_cdv, s_d, &s_fkey,
@@ -473,8 +547,42 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     DSTAMP(tsf);
     // the exact current d of the cached cells (the fast path computed them
     // before it failed): a lower bound of the new max(d)
-    const int theta0 = mode == 2 ? (int)full[9 + 2 * fi] : ((s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0);
-    if (!fast) {
+    const int theta0 = mode >= 2 ? (int)full[9 + 2 * fi] : ((s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0);
+    bool need_cb = true;  // the map's bitboard in LDS
+    if (mode == 3) {
+      // ---- merge the parts' partials: the best key, the raw target d (in
+      // the output buffers), the strip maxima, the cache candidates
+      __syncthreads();  // the item's LDS scalars are initialised
+      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
+      const unsigned long long gk = s.dist_gkey[ea];
+      const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
+      for (int t = tid; t < T; t += kDtThreads)
+        s_d[t] = (int)(t < 5 ? pre_out[(size_t)ea * 8 + 1 + t] : dist_obs[(size_t)ea * E * E + (t - 5)]);
+      for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
+        s_smax[st] = s.dist_sm[(size_t)ea * kMaxTrack + st];
+      if (gk != 0 && total <= (uint32_t)kGCand)
+        for (int k = tid; k < (int)total; k += kDtThreads) {
+          const int2 c = s.dist_gcand[(size_t)ea * kGCand + k];
+          if (c.y >= thr) {
+            const int j = atomicAdd(&s_ccount, 1);
+            if (j < kDistK) {
+              s_ccell[j] = c.x;
+              s_cdv[j] = (uint16_t)c.y;
+            }
+          }
+        }
+      __syncthreads();
+      if (tid == 0) {
+        s_key = gk;
+        s_cov = gk != 0;  // a covered map's key is nonzero (its far or cell field)
+        if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
+        s.dist_gkey[ea] = 0;  // zero for the map's next split transform
+        s.dist_gcnt[ea] = 0;
+      }
+      __syncthreads();
+      need_cb = s_cov && s.dist_ch && !(kOnePass && theta0 > 0 && s_ccount <= kDistK);
+    }
+    if (!fast && need_cb) {
       for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
       {
         // the agent's tiles (coalesced loads) scattered as row bytes into map
@@ -723,7 +831,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       }
     };
-    const int nstrips = (cov && !fast) ? nstrips_all : 0;
+    const int nstrips = (cov && !fast && mode != 3) ? nstrips_all : 0;
     // The cache's cells in the same pass: every cell with d >= M - kDistT
     // (M = the new max, known only at the end) has d >= any lower bound of
     // M, less kDistT.  Bounds: theta0 and the strips' maxima so far (s_smax
@@ -787,9 +895,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                             ((unsigned long long)ubest << 16) | (unsigned long long)vbest);
     }
     __syncthreads();
-    if (mode == 2 && S > 1 && !fast) {
+    if (mode == 2 && S > 1) {
       // ---- a part: publish the best key, the targets it holds (raw d in
-      // the output buffers), its strips' maxima and its cache candidates
+      // the output buffers), its strips' maxima and its cache candidates;
+      // mode 3 finalises the map
       if (tid == 0 && s_key) atomicMax(s.dist_gkey + ea, s_key);
       for (int t = tid; t < T; t += kDtThreads)
         if (s_d[t] >= 0) {
@@ -807,49 +916,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           for (int k = tid; k < n; k += kDtThreads)
             if (base + k < (uint32_t)kGCand) s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
       }
-      __threadfence();
-      __syncthreads();
-      if (tid == 0) s_last = atomicAdd(s.dist_gdone + ea, 1u) == (uint32_t)(S - 1);
-      __syncthreads();
-      if (!s_last) {
-        __syncthreads();  // the LDS is reused by the next item
-        continue;
-      }
-      // ---- the last part: merge every part's partials into this workgroup's
-      // state, then finalise the map as a whole-map workgroup does
-      __threadfence();
-      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
-      const unsigned long long gk = s.dist_gkey[ea];
-      const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
-      for (int t = tid; t < T; t += kDtThreads)
-        s_d[t] = (int)(t < 5 ? pre_out[(size_t)ea * 8 + 1 + t] : dist_obs[(size_t)ea * E * E + (t - 5)]);
-      for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
-        s_smax[st] = s.dist_sm[(size_t)ea * kMaxTrack + st];
-      __syncthreads();  // every part's own s_key / s_ccount reads are done
-      if (tid == 0) {
-        s_key = gk;
-        s_ccount = 0;
-      }
-      __syncthreads();
-      if (total <= (uint32_t)kGCand)
-        for (int k = tid; k < (int)total; k += kDtThreads) {
-          const int2 c = s.dist_gcand[(size_t)ea * kGCand + k];
-          if (c.y >= thr) {
-            const int j = atomicAdd(&s_ccount, 1);
-            if (j < kDistK) {
-              s_ccell[j] = c.x;
-              s_cdv[j] = (uint16_t)c.y;
-            }
-          }
-        }
-      __syncthreads();
-      if (tid == 0) {
-        if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
-        s.dist_gkey[ea] = 0;  // zero for the map's next split transform
-        s.dist_gdone[ea] = 0;
-        s.dist_gcnt[ea] = 0;
-      }
-      __syncthreads();
+      __syncthreads();  // the LDS is reused by the next item
+      continue;
     }
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
@@ -997,6 +1065,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   __shared__ uint32_t s_served, s_nf, s_fbase, s_nc;
   __shared__ uint2 s_fl[kFastBuf];     // this workgroup's maps for the full list
   __shared__ uint32_t s_cl[kFastBuf];  // this chunk's maps with a cache
+  __shared__ uint32_t s_span[2 * kSpan];
   const int tid = threadIdx.x;
   const int T = 5 + s.E * s.E;
   const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
@@ -1038,7 +1107,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
       bool tried = false;
       cache_try<kFastThreads>(s, pad, T, pp.x, pp.y, s.freem + (size_t)ea * s.MT, ccnt, h0.z, h0.w, h1.x, h1.y, ft,
                               s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, cdv, s_dyn, &s_fkey,
-                              &s_ffail, tried);
+                              &s_ffail, tried, s_span);
       if (tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT) {
         cache_serve<kFastThreads>(s, T, ea, s_fkey, ccnt, cM0, cdv, s_dyn, pre_out, dist_obs, nullptr);
         if (tid == 0) ++s_served;
@@ -1103,8 +1172,9 @@ hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float*
 // (mc_env_kernel.hip dist_window) and lists only the maps with an unknown M
 // or a target the block cannot settle.  With the top-cell cache, the listed
 // maps first try the cache (mode 1) and the rest run split over workgroups
-// (mode 2; `full`: the full list); without it, each listed map runs whole
-// (mode 0).  The grids are fixed (hipGraph capture) and stride.
+// (mode 2; `full`: the full list), finalised by mode 3 when split over more
+// than one part; without it, each listed map runs whole (mode 0).  The grids
+// are fixed (hipGraph capture) and stride.
 // --------------------------------------------------------------------------
 hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* dist_obs,
                               uint32_t* list, uint32_t* count, uint32_t* full, hipStream_t stream) {
@@ -1116,7 +1186,9 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
                      pre_out, dist_obs, list, count, full);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, 2048, 2, full, stream);
+  e = launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, 2048, 2, full, stream);
+  if (e != hipSuccess) return e;
+  return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, grid < 1024 ? grid : 1024, 3, full, stream);
 }
 
 }  // namespace mc

@@ -141,10 +141,9 @@ struct State {
   // the last full transform; d only decreases), valid while the cache is
   uint16_t* dist_sm;
   // with the cache: the split full transform's per-map partials (mc_dist.hip
-  // mode 2; zero between uses): the best key, the parts done, the candidate
-  // cells published and the candidates [B][N][kDistK] (cell, d)
+  // modes 2 / 3; zero between uses): the best key, the candidate cells
+  // published and the candidates [B][N][4 * kDistK] (cell, d)
   unsigned long long* dist_gkey;
-  uint32_t* dist_gdone;
   uint32_t* dist_gcnt;
   int2* dist_gcand;
   // episode record, written when an env reports done (before an auto-reset

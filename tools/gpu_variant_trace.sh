@@ -18,7 +18,7 @@ K = int(sys.argv[2])
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 rows = [r for r in rows if "rocclr" not in r["Kernel_Name"] and "random_actions" not in r["Kernel_Name"]
         and "at::" not in r["Kernel_Name"]]
-env = [i for i, r in enumerate(rows) if "env_kernel" in r["Kernel_Name"]]
+env = [i for i, r in enumerate(rows) if "env_kernel" in r["Kernel_Name"] or "sg_step" in r["Kernel_Name"]]
 first = env[-K]  # the timed steps: from the K-th last env kernel on
 d = collections.defaultdict(float)
 for r in rows[first:]:
