@@ -87,7 +87,10 @@ constexpr int kMaxTrack = kDistStrips;         // strips whose max(d) the cache 
 #define MC_DIST_ONEPASS 1
 #endif
 constexpr bool kOnePass = MC_DIST_ONEPASS != 0;
-constexpr int kFastTiles = 2048;               // tiles the cache fast path stages (box + 25 around the robot)
+#ifndef MC_FAST_TILES  // build knob (A/B): tiles the cache fast path stages (box + 25 around the robot)
+#define MC_FAST_TILES 2048
+#endif
+constexpr int kFastTiles = MC_FAST_TILES;
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 constexpr u16x2 kNone2 = {0xFFFF, 0xFFFF};
 constexpr u16x2 kRowOff2 = {kRowOff, kRowOff};
@@ -230,12 +233,13 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
 // `span` (optional, 2 * kSpan words): the staged box's covered extent per
 // row and per column, for the cells outside the box's column or row band.
 // Ends with a barrier.
-constexpr int kSpan = 512;  // box rows / columns the span arrays hold
+constexpr int kSpan = 256;  // box rows / columns the span arrays hold
 template <int NTH>
 __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px, int py, const uint64_t* free_t,
                                           int ccnt, int bx0, int by0, int bx1, int by1, uint64_t* ft,
                                           const int32_t* cc, const int32_t* cd, uint16_t* cdv, int* s_d,
-                                          uint32_t* fkey, int* ffail, bool& tried, uint32_t* span = nullptr) {
+                                          uint32_t* fkey, int* ffail, bool& tried, uint32_t* span = nullptr,
+                                          uint64_t* ts = nullptr) {
   const int tid = threadIdx.x, E = s.E;
   const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
   const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
@@ -247,6 +251,16 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
   const int rti0 = (tx_c >> 3) - 2, rtj0 = (ty_c >> 3) - 2;
   tried = nt + 25 <= kFastTiles;
   if (!tried) return;
+  // the thread's cached cells (cell, d): loads in flight with the tiles'
+  constexpr int KC = (kDistK + NTH - 1) / NTH;
+  int32_t pcw[KC], pcd[KC];
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int k = tid + j * NTH;
+    pcw[j] = k < ccnt ? cc[k] : 0;
+    pcd[j] = k < ccnt ? cd[k] : 0;
+  }
+  for (int t = tid; t < T; t += NTH) s_d[t] = kInf;
   for (int i = tid; i < nt + 25; i += NTH) {
     int ti, tj;
     if (i < nt) {
@@ -264,6 +278,7 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     ft[i] = t;
   }
   __syncthreads();
+  if (ts) DSTAMP(ts[0]);
   // the staged box (tile-aligned): rows [X0, X0 + 8 nbr), columns [Y0, Y0 + 8 nbc)
   const int X0 = 8 * ti0, Y0 = 8 * tj0, NR = 8 * nbr, NC = 8 * nbc;
   const bool rspan = span && nt > 0 && NR <= kSpan, cspan = span && nt > 0 && NC <= kSpan;
@@ -299,10 +314,13 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     __syncthreads();
   }
   uint32_t mykey = 0;
-  for (int k = tid; k < ccnt; k += NTH) {
-    const int32_t cw = cc[k];
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int k = tid + j * NTH;
+    if (k >= ccnt) break;
+    const int32_t cw = pcw[j];
     const int cx = witness_x(cw), cy = witness_y(cw);
-    int d = cd[k];
+    int d = pcd[j];
     // only box tiles inside the cell's L1 ball of radius d can lower it (a
     // cell at least d from the box keeps its d): tile rows outward from the
     // cell's, each row's columns limited by the radius left (d shrinks as
@@ -361,12 +379,12 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     cdv[k] = d;
     mykey = max(mykey, ((uint32_t)d << 16) | (uint32_t)k);
   }
+  if (ts) DSTAMP(ts[1]);
   mykey = wave_max_u32(mykey);
   if ((tid & 63) == 0) atomicMax(fkey, mykey);
-  for (int t = tid; t < T; t += NTH) {
-    // target t, map coordinates: [0, 5) the end cells of the next step at the
-    // quirk index (padded-grid x, y, no pad offset), then the crop
-    int tx, ty;
+  // target t, map coordinates: [0, 5) the end cells of the next step at the
+  // quirk index (padded-grid x, y, no pad offset), then the crop
+  auto target_cell = [&](int t, int& tx, int& ty) {
     if (t >= 5) {
       const int r = (t - 5) / E;
       tx = px - s.ego + r;
@@ -375,19 +393,24 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
       tx = px + (t == 1 ? 1 : (t == 3 ? -1 : 0)) - pad;
       ty = py + (t == 2 ? 1 : (t == 4 ? -1 : 0)) - pad;
     }
-    int d = kInf;
-    {  // the target's own tile first: a covered target ends the search at once
-      const int r = min(max((tx >> 3) - rti0, 0), 4), c = min(max((ty >> 3) - rtj0, 0), 4);
-      d = tile_min_dist(ft[nt + 5 * r + c], 8 * (rti0 + r), 8 * (rtj0 + c), tx, ty, d);
-    }
-    for (int i = 0; i < 25; ++i) {
-      const int r = i / 5;
-      d = tile_min_dist(ft[nt + i], 8 * (rti0 + r), 8 * (rtj0 + i - 5 * r), tx, ty, d);
-    }
-    s_d[t] = d;
+  };
+  // d of each target: its 25 tiles as (target, tile) items over the threads
+  // (a thread per target walking 25 tiles was the try's latency chain), the
+  // minimum per target in LDS
+  for (int i = tid; i < 25 * T; i += NTH) {
+    const int t = i / 25, j = i - 25 * t, r = j / 5;
+    int tx, ty;
+    target_cell(t, tx, ty);
+    const int d = tile_min_dist(ft[nt + j], 8 * (rti0 + r), 8 * (rtj0 + j - 5 * r), tx, ty, kInf);
+    if (d < kInf) atomicMin(&s_d[t], d);
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += NTH) {
+    int tx, ty;
+    target_cell(t, tx, ty);
     // exact only if no cell outside the 40 x 40 block can be nearer
     const int b = min(min(tx - 8 * rti0, 8 * rti0 + 39 - tx), min(ty - 8 * rtj0, 8 * rtj0 + 39 - ty)) + 1;
-    if (d > b) *ffail = 1;
+    if (s_d[t] > b) *ffail = 1;
   }
   __syncthreads();
 }
@@ -553,7 +576,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       // ---- merge the parts' partials: the best key, the raw target d (in
       // the output buffers), the strip maxima, the cache candidates
       __syncthreads();  // the item's LDS scalars are initialised
-      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
+      const uint32_t total = s.dist_gcnt[ea];  // every part published its candidates
       const unsigned long long gk = s.dist_gkey[ea];
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
       for (int t = tid; t < T; t += kDtThreads)
@@ -580,10 +603,11 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s.dist_gcnt[ea] = 0;
       }
       __syncthreads();
-      need_cb = s_cov && s.dist_ch && !(kOnePass && theta0 > 0 && s_ccount <= kDistK);
+      need_cb = s_cov && s_ccount > kDistK;  // an overflowed list: the second pass
     }
     if (!fast && need_cb) {
-      for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
+      if (mode != 3)  // (mode 3 holds the parts' targets)
+        for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
       {
         // the agent's tiles (coalesced loads) scattered as row bytes into map
         // rows in the strip area (free until the strips start): byte tj of map
@@ -850,8 +874,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     int runmax = 0;
     uint64_t ran = 0;  // strips transformed (their s_smax are exact maxima)
     const int s_from = nstrips > 0 ? st_lo : 0, s_to = nstrips > 0 ? st_hi : 0;
-    if (s_from > 0 && s_from < s_to) {  // a part's first strip: each row's last covered column left of it
-      const int c0 = s_from * kStrip, w = c0 >> 6;
+    // a part's first strip st0: each row's last covered column left of it
+    auto carry_in = [&](int st0) {
+      lastL[0] = lastL[1] = -kInf;
+      nrw[0] = nrw[1] = -1;
+      if (st0 == 0) return;
+      const int c0 = st0 * kStrip, w = c0 >> 6;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int u = tid + q * kDtThreads;
@@ -861,21 +889,26 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         while (!m && k > 0) m = Cb[u * RW + --k];
         if (m) lastL[q] = 64 * k + 63 - __clzll((unsigned long long)m);
       }
-    }
+    };
+    // a strip the pass skips: only its rows' last covered column is carried
+    auto carry_over = [&](int st) {
+      const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int u = tid + q * kDtThreads;
+        if (u >= RX) continue;
+        const uint32_t sb = (uint32_t)(Cb[u * RW + w] >> (32 * h));
+        if (sb) lastL[q] = c0 + 31 - __clz(sb);
+      }
+    };
+    if (s_from > 0 && s_from < s_to) carry_in(s_from);
     for (int st = s_from; st < s_to; ++st) {
       if (st - 2 >= s_from && st - 2 < kMaxTrack && ((ran >> (st - 2)) & 1ull)) runmax = max(runmax, s_smax[st - 2]);
       if (prune) {
         const int c0 = st * kStrip, bound = smb[st];
         if (bound < theta0 - kDistT && !(c0 + kStrip > tv_lo && c0 <= tv_hi)) {
           if (tid == 0) s_smax[st] = bound;
-          const int w = c0 >> 6, h = (c0 >> 5) & 1;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int u = tid + q * kDtThreads;
-            if (u >= RX) continue;
-            const uint32_t sb = (uint32_t)(Cb[u * RW + w] >> (32 * h));
-            if (sb) lastL[q] = c0 + 31 - __clz(sb);
-          }
+          carry_over(st);
           continue;
         }
       }
@@ -907,14 +940,35 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
         if ((ran >> st) & 1ull) s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
-      if (kOnePass && theta0 > 0) {
-        const int n = s_ccount;
-        if (tid == 0) s_base = atomicAdd(s.dist_gcnt + ea, (uint32_t)(n <= kDistK ? n : kGCand + 1));
+      if (!(kOnePass && theta0 > 0) && s.dist_ch && nstrips > 0) {
+        // no one-pass list (no theta0): the part's own cache candidates in a
+        // second pass over its strips, from the best lower bound of the new
+        // max at hand -- its own max, or the global key so far (any value
+        // read is a max of exact maxima)
+        const unsigned long long gk = __hip_atomic_load(s.dist_gkey + ea, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int thr = max((int)(s_key >> 48), (int)(gk >> 48)) - kDistT;
+        if (thr >= 0) {
+          carry_in(st_lo);
+          for (int st = st_lo; st < st_hi; ++st) {
+            if (st >= kMaxTrack || s_smax[st] >= thr) strip(st, thr, -1);
+            else carry_over(st);
+          }
+        } else if (tid == 0) {
+          s_ccount = kDistK + 1;  // no useful bound: mode 3's second pass
+        }
         __syncthreads();
-        const uint32_t base = s_base;
-        if (n <= kDistK)
-          for (int k = tid; k < n; k += kDtThreads)
-            if (base + k < (uint32_t)kGCand) s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
+      }
+      if (s.dist_ch) {
+        const int n = s_ccount;
+        if (n > 0) {
+          if (tid == 0) s_base = atomicAdd(s.dist_gcnt + ea, (uint32_t)(n <= kDistK ? n : kGCand + 1));
+          __syncthreads();
+          const uint32_t base = s_base;
+          if (n <= kDistK)
+            for (int k = tid; k < n; k += kDtThreads)
+              if (base + k < (uint32_t)kGCand)
+                s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
+        }
       }
       __syncthreads();  // the LDS is reused by the next item
       continue;
@@ -934,7 +988,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         // the cache pass: every cell with d >= M - kDistT (strips whose max
         // reaches it; the others only carry their last covered column)
         int cnt = -1;
-        const bool main_ok = kOnePass && theta0 > 0 && s_ccount <= kDistK;  // the main pass's list holds them all
+        // the main pass's list (mode 3: the parts' lists) holds them all
+        const bool main_ok = (mode == 3 || (kOnePass && theta0 > 0)) && s_ccount <= kDistK;
         if (cov && M >= 0 && main_ok) {
           const int thr = M - kDistT, n = s_ccount;
           for (int k = tid; k < n; k += kDtThreads)
@@ -952,21 +1007,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           if (tid == 0) s_ccount = 0;
           __syncthreads();
           const int thr = M - kDistT;
-          lastL[0] = lastL[1] = -kInf;
-          nrw[0] = nrw[1] = -1;
+          carry_in(0);
           for (int st = 0; st < nstrips_all; ++st) {
-            if (st >= kMaxTrack || s_smax[st] >= thr) {
-              strip(st, thr, -1);
-            } else {
-              const int c0 = st * kStrip, w = c0 >> 6, h = (c0 >> 5) & 1;
-#pragma unroll
-              for (int q = 0; q < 2; ++q) {
-                const int u = tid + q * kDtThreads;
-                if (u >= RX) continue;
-                const uint32_t sb = (uint32_t)(Cb[u * RW + w] >> (32 * h));
-                if (sb) lastL[q] = c0 + 31 - __clz(sb);
-              }
-            }
+            if (st >= kMaxTrack || s_smax[st] >= thr) strip(st, thr, -1);
+            else carry_over(st);
           }
           __syncthreads();
           cnt = s_ccount <= kDistK ? s_ccount : -1;
@@ -1049,7 +1093,17 @@ size_t dist_static_lds_bytes() {
 // transform kernel's LDS admits two workgroups per CU); a map it cannot
 // serve goes to the full list with its theta0 (the exact max of its cached
 // cells' d, a lower bound of the new max(d); 0 without a try).
-constexpr int kFastThreads = 256;
+// Build knobs (A/B, profiles/r4/c5_fast/): threads per workgroup and grid.
+// A wave per map (64 threads, 512 tiles, grid 4096) was slower: 52.9 vs
+// 28.1 us per step at the C5 steady state, the try's time scaling with the
+// threads it has
+#ifndef MC_FAST_THREADS
+#define MC_FAST_THREADS 256
+#endif
+#ifndef MC_FAST_GRID
+#define MC_FAST_GRID 2048
+#endif
+constexpr int kFastThreads = MC_FAST_THREADS;
 constexpr int kFastBuf = 128;  // full-list entries a workgroup buffers before one atomic
 
 __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pad, float* __restrict__ pre_out,
@@ -1069,6 +1123,8 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   const int tid = threadIdx.x;
   const int T = 5 + s.E * s.E;
   const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
+  uint64_t tk0 = 0;
+  DSTAMP(tk0);
   if (tid == 0) s_served = s_nf = 0;
   // a contiguous share of the list per workgroup, kFastBuf maps at a time:
   // one thread per map reads its cache header (a map without a cache goes
@@ -1094,6 +1150,9 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
     const uint32_t nc = s_nc;
     for (uint32_t j = 0; j < nc; ++j) {
       const uint32_t ea = s_cl[j];
+      uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
+      uint64_t tsv[2] = {0, 0};
+      DSTAMP(tm0);
       const int4 h0 = reinterpret_cast<const int4*>(s.dist_ch + (size_t)ea * 8)[0];
       const int2 h1 = reinterpret_cast<const int2*>(s.dist_ch + (size_t)ea * 8)[2];
       const int ccnt = h0.x, cM0 = h0.y;
@@ -1107,13 +1166,38 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
       bool tried = false;
       cache_try<kFastThreads>(s, pad, T, pp.x, pp.y, s.freem + (size_t)ea * s.MT, ccnt, h0.z, h0.w, h1.x, h1.y, ft,
                               s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, cdv, s_dyn, &s_fkey,
-                              &s_ffail, tried, s_span);
-      if (tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT) {
+                              &s_ffail, tried, s_span,
+#ifdef MC_DIST_STAMPS
+                              tsv
+#else
+                              nullptr
+#endif
+      );
+      DSTAMP(tm1);
+      const bool served = tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
+      if (served) {
         cache_serve<kFastThreads>(s, T, ea, s_fkey, ccnt, cM0, cdv, s_dyn, pre_out, dist_obs, nullptr);
         if (tid == 0) ++s_served;
       } else if (tid == 0) {
         to_full(ea, tried ? (s_fkey >> 16) : 0u);
       }
+      DSTAMP(tm2);
+#ifdef MC_DIST_STAMPS
+      // a served map: the wait from the kernel's start, the try, the serve
+      // (the transform kernels stamp the maps they run)
+      if (served && tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u) {
+        auto f16 = [](uint64_t a, uint64_t b) -> uint64_t {
+          const uint64_t d = (b - a) >> 4;
+          return d < 0xFFFFull ? d : 0xFFFFull;
+        };
+        // (diagnostic: the try's phases -- staging, spans + cells, targets)
+        s.stamps[ea] = f16(tm0, tsv[0]) | (f16(tsv[0], tsv[1]) << 16) | (f16(tsv[1], tm1) << 32) | (1ull << 48) |
+                       (1ull << 51);
+        (void)tk0; (void)tm2;
+      }
+#else
+      (void)tm0; (void)tm1; (void)tm2; (void)tk0; (void)tsv;
+#endif
       __syncthreads();  // the LDS is reused by the next map
     }
   }
@@ -1182,7 +1266,8 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
   const unsigned grid = (unsigned)(maps < 2048 ? maps : 2048);
   if (!full || !s.dist_ch)
     return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, 0, nullptr, stream);
-  hipLaunchKernelGGL(dist_fast_kernel, dim3(grid), dim3(kFastThreads), (size_t)(5 + s.E * s.E) * 4, stream, s, pad,
+  const unsigned fgrid = (unsigned)(maps < MC_FAST_GRID ? maps : MC_FAST_GRID);
+  hipLaunchKernelGGL(dist_fast_kernel, dim3(fgrid), dim3(kFastThreads), (size_t)(5 + s.E * s.E) * 4, stream, s, pad,
                      pre_out, dist_obs, list, count, full);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

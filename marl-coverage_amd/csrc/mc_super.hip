@@ -940,62 +940,6 @@ __host__ __device__ inline size_t erode_lds_bytes(int W, int L) {
   return 2 * nw * 8 + (((size_t)W * L + 15) & ~(size_t)15) + (((size_t)(W + L + 1) * 4 + 15) & ~(size_t)15);
 }
 
-// The distance layer from the per-cell d (d8, LDS; every writer's d8 stores
-// are behind a barrier) and max(d) M: the value LUT, dist_M, then the changed
-// region or the whole layer (sg_erode_kernel, sg_erode_wave_kernel).
-__device__ __forceinline__ void write_dist_layer(const SState& s, int e, int tid, int NT, const uint8_t* d8,
-                                                 float* lut, int M, int M_old, bool was_full, const int* s_px,
-                                                 const int* s_py) {
-  const int W = s.W, L = s.L;
-  const size_t WL = (size_t)W * L;
-  float* out = s.dist_plane + (size_t)e * WL;
-  const float Mf = (float)M;
-  for (int d = tid; d <= M; d += NT) lut[d] = dist_value((float)d, Mf);
-  if (tid == 0) s.dist_M[e] = M;
-  // Since the layer was last written only this step's sensing changed the
-  // map: newly covered cells n lie in the robots' windows (|n - p_i| <= r,
-  // Chebyshev), and a cell's d changes only if its nearest source was such a
-  // cell, i.e. |c - n|_1 <= d_old(c) <= M_old.  So with max(d) unchanged every
-  // changed value lies within r + M_old of a robot, and the rest of the layer
-  // already holds the exact new values.  A changed max, a full-rewrite flag
-  // (reset / state upload) or MARLCOV_SG_FULL_DIST rewrites the whole layer.
-  const int h = s.r + (M_old > 0 ? M_old : 0) + 1, side = 2 * h + 1;
-  const bool all = was_full || s.dist_full || M != M_old || M_old < 0 ||
-                   (size_t)s.N * side * side >= WL;
-  __syncthreads();
-  if (!all) {
-    // idx = (i * side + rr) * side + cc, divided once and then advanced by NT
-    // with carries (each digit step is < side, so one subtraction each)
-    const int per = side * side;
-    const int q_nt = NT / side, st_cc = NT - q_nt * side;
-    const int st_i = q_nt / side, st_rr = q_nt - st_i * side;
-    int i = tid / per;
-    int rr = (tid - i * per) / side;
-    int cc = tid - i * per - rr * side;
-    for (int idx = tid; idx < s.N * per; idx += NT) {
-      const int u = s_px[i] - h + rr;
-      const int v = s_py[i] - h + cc;
-      if (u >= 0 && u < W && v >= 0 && v < L) out[(size_t)u * L + v] = lut[d8[(size_t)u * L + v]];
-      cc += st_cc;
-      int c = cc >= side;
-      cc -= c ? side : 0;
-      rr += st_rr + c;
-      c = rr >= side;
-      rr -= c ? side : 0;
-      i += st_i + c;
-    }
-  } else if ((L & 3) == 0) {
-    const uint32_t* d4 = reinterpret_cast<const uint32_t*>(d8);
-    float4* o4 = reinterpret_cast<float4*>(out);
-    for (size_t g = tid; g < WL / 4; g += NT) {
-      const uint32_t q = d4[g];
-      o4[g] = make_float4(lut[q & 255u], lut[(q >> 8) & 255u], lut[(q >> 16) & 255u], lut[q >> 24]);
-    }
-  } else {
-    for (size_t i = tid; i < WL; i += NT) out[i] = lut[d8[i]];
-  }
-}
-
 // Distance layer by bit-parallel erosion (maps with W + L <= 257 whose
 // planes fit LDS; every BASELINE-sized map).  With C = the sensed cells and
 // cells outside the grid counting as non-sources (OpenCV's border), the L1
@@ -1082,131 +1026,51 @@ __global__ __launch_bounds__(256) void sg_erode_kernel(SState s) {
       nxt = t;
     }
   }
+  const float Mf = (float)M;
+  for (int d = tid; d <= M; d += NT) lut[d] = dist_value((float)d, Mf);
+  if (tid == 0) s.dist_M[e] = M;
+  // Since the layer was last written only this step's sensing changed the
+  // map: newly covered cells n lie in the robots' windows (|n - p_i| <= r,
+  // Chebyshev), and a cell's d changes only if its nearest source was such a
+  // cell, i.e. |c - n|_1 <= d_old(c) <= M_old.  So with max(d) unchanged every
+  // changed value lies within r + M_old of a robot, and the rest of the layer
+  // already holds the exact new values.  A changed max, a full-rewrite flag
+  // (reset / state upload) or MARLCOV_SG_FULL_DIST rewrites the whole layer.
+  const int h = s.r + (M_old > 0 ? M_old : 0) + 1, side = 2 * h + 1;
+  const bool all = was_full || s.dist_full || M != M_old || M_old < 0 ||
+                   (size_t)s.N * side * side >= WL;
   __syncthreads();
-  write_dist_layer(s, e, tid, NT, d8, lut, M, M_old, was_full, s_px, s_py);
-}
-
-// The erosion in one wave per env, the bitboard in registers (maps with L <=
-// 128, L % 4 == 0 and W <= 4 * 64 / RW rows; sg_c2's 128 x 128): lane l holds
-// column word w = l % RW of rows 4 g .. 4 g + 3, g = l / RW.  A step needs the
-// row above the lane's first and below its last (ds_bpermute from lanes l -+
-// RW) and, with RW = 2, the other word's edge bits (DPP quad_perm, lane l ^ 1).
-// No barrier per step (sg_erode_kernel: one per step across 4 waves).  d is
-// kept bit-sliced: a cell leaving at step k ORs its word into the planes of
-// k + 1's set bits; the planes become d8 bytes (4 cells per u32) at the end.
-constexpr int kWaveRows = 4;
-__host__ __device__ inline bool erode_wave_fits(int W, int L) {
-  const int RW = (L + 63) / 64;
-  return L <= 128 && (L & 3) == 0 && W <= kWaveRows * (64 / RW) && W + L <= 257;
-}
-__host__ __device__ inline size_t erode_wave_lds_bytes(int W, int L) {
-  return (((size_t)W * L + 15) & ~(size_t)15) + (((size_t)(W + L + 1) * 4 + 15) & ~(size_t)15);
-}
-__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int src) {  // v of lane src (0 .. 63)
-  const int a = src << 2;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-template <int RWT>
-__global__ __launch_bounds__(64) void sg_erode_wave_kernel(SState s) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int s_px[kMaxAgents], s_py[kMaxAgents];
-  constexpr int R = kWaveRows, G = 64 / RWT;
-  const int e = blockIdx.x, lane = threadIdx.x;
-  const int W = s.W, L = s.L;
-  const size_t WL = (size_t)W * L;
-  const bool was_full = s.full[e] != 0;  // read by every lane before it is cleared
-  const int M_old = s.dist_M[e];
-  if (lane < s.N) {
-    s_px[lane] = s.pos[((size_t)e * s.N + lane) * 2];
-    s_py[lane] = s.pos[((size_t)e * s.N + lane) * 2 + 1];
-  }
-  if (was_full) write_full_layers(s, e, lane, 64, s_px, s_py);
-  uint8_t* d8 = reinterpret_cast<uint8_t*>(smem);
-  float* lut = reinterpret_cast<float*>(smem + ((WL + 15) & ~(size_t)15));
-  const int w = RWT == 2 ? (lane & 1) : 0, g = RWT == 2 ? (lane >> 1) : lane, u0 = g * R;
-  const uint64_t inval = (w == RWT - 1 && (L & 63)) ? ~low_mask(L & 63) : 0ull;  // bits >= L
-  const uint64_t* cov = s.cov + (size_t)e * W * RWT;
-  uint64_t c[R], pad[R];  // pad: bits outside the grid (never sources, never leave)
-  bool src = false, anyc = false;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int u = u0 + i;
-    pad[i] = u < W ? inval : ~0ull;
-    const uint64_t v = u < W ? cov[(size_t)u * RWT + w] & ~inval : 0ull;
-    c[i] = v | pad[i];
-    src |= c[i] != ~0ull;
-    anyc |= v != 0ull;
-  }
-  const bool any_src = __ballot(src) != 0ull, any_cov = __ballot(anyc) != 0ull;
-  if (!any_src) {  // no source cell: SciPy's -1 everywhere -> 1 - (-1)
-    float4* o4 = reinterpret_cast<float4*>(s.dist_plane + (size_t)e * WL);
-    for (size_t i = lane; i < WL / 4; i += 64) o4[i] = make_float4(2.0f, 2.0f, 2.0f, 2.0f);
-    if (lane == 0) s.dist_M[e] = -2;
-    return;
-  }
-  uint64_t pl[8][R];  // bit b of each cell's d (d <= W + L - 2 < 256)
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-#pragma unroll
-    for (int i = 0; i < R; ++i) pl[b][i] = 0ull;
-  int M = 0;
-  if (any_cov) {
-    for (int k = 0;; ++k) {
-      // every lane runs both permutes (a source lane must be active)
-      const uint64_t upv = lane_u64(c[R - 1], max(lane - RWT, 0)), dnv = lane_u64(c[0], min(lane + RWT, 63));
-      const uint64_t upn = g > 0 ? upv : ~0ull, dnn = g < G - 1 ? dnv : ~0ull;
-      uint32_t ob = 0xFFFFFFFFu;  // the other word's edge bits (none: non-source)
-      if constexpr (RWT == 2) {
-        uint32_t eb = 0;  // bit 2i: row i's bit 63, bit 2i + 1: its bit 0
-#pragma unroll
-        for (int i = 0; i < R; ++i) eb |= ((uint32_t)(c[i] >> 63) << (2 * i)) | ((uint32_t)(c[i] & 1ull) << (2 * i + 1));
-        ob = (uint32_t)__builtin_amdgcn_mov_dpp((int)eb, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-      }
-      const uint32_t dk = (uint32_t)(k + 1);
-      bool nz = false;
-      uint64_t n[R];
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const uint64_t up = i > 0 ? c[i - 1] : upn;
-        const uint64_t dn = i < R - 1 ? c[i + 1] : dnn;
-        const uint64_t lb = (RWT == 2 && w == 1) ? (uint64_t)((ob >> (2 * i)) & 1u) : 1ull;               // word w-1, bit 63
-        const uint64_t rb = (RWT == 2 && w == 0) ? (uint64_t)((ob >> (2 * i + 1)) & 1u) << 63 : 1ull << 63;  // word w+1, bit 0
-        n[i] = (c[i] & up & dn & ((c[i] << 1) | lb) & ((c[i] >> 1) | rb)) | pad[i];
-        const uint64_t leave = c[i] & ~n[i];
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if ((dk >> b) & 1u) pl[b][i] |= leave;
-        nz |= (n[i] & ~pad[i]) != 0ull;
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i) c[i] = n[i];
-      if (!__ballot(nz)) {
-        M = k + 1;
-        break;
-      }
+  if (!all) {
+    // idx = (i * side + rr) * side + cc, divided once and then advanced by NT
+    // with carries (each digit step is < side, so one subtraction each)
+    const int per = side * side;
+    const int q_nt = NT / side, st_cc = NT - q_nt * side;
+    const int st_i = q_nt / side, st_rr = q_nt - st_i * side;
+    int i = tid / per;
+    int rr = (tid - i * per) / side;
+    int cc = tid - i * per - rr * side;
+    for (int idx = tid; idx < s.N * per; idx += NT) {
+      const int u = s_px[i] - h + rr;
+      const int v = s_py[i] - h + cc;
+      if (u >= 0 && u < W && v >= 0 && v < L) out[(size_t)u * L + v] = lut[d8[(size_t)u * L + v]];
+      cc += st_cc;
+      int c = cc >= side;
+      cc -= c ? side : 0;
+      rr += st_rr + c;
+      c = rr >= side;
+      rr -= c ? side : 0;
+      i += st_i + c;
     }
-  }
-  // the planes as d bytes, 4 cells per u32: nibble q of plane b spread to bit
-  // b of 4 bytes ((x * 0x204081) & 0x01010101 moves bit j of a nibble to byte j)
-  const int nb = M > 0 ? 32 - __clz(M) : 0;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int u = u0 + i;
-    if (u >= W) continue;
-    uint32_t* drow = reinterpret_cast<uint32_t*>(d8 + (size_t)u * L + 64 * w);
-    const int nq = min(16, (L - 64 * w) >> 2);
-    for (int q = 0; q < nq; ++q) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int b = 0; b < 8; ++b)
-        if (b < nb) v |= (((uint32_t)(pl[b][i] >> (4 * q)) & 0xFu) * 0x204081u & 0x01010101u) << b;
-      drow[q] = v;
+  } else if ((L & 3) == 0) {
+    const uint32_t* d4 = reinterpret_cast<const uint32_t*>(d8);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    for (size_t g = tid; g < WL / 4; g += NT) {
+      const uint32_t q = d4[g];
+      o4[g] = make_float4(lut[q & 255u], lut[(q >> 8) & 255u], lut[(q >> 16) & 255u], lut[q >> 24]);
     }
+  } else {
+    for (size_t i = tid; i < WL; i += NT) out[i] = lut[d8[i]];
   }
-  __syncthreads();
-  write_dist_layer(s, e, lane, 64, d8, lut, M, M_old, was_full, s_px, s_py);
 }
 
 // Distance layer by separable sweeps (any map up to kMaxSide): a row pass
@@ -1373,7 +1237,6 @@ struct SgEnv {
   int pitch = 0;      // u16 elements per distance-plane row
   bool lds = true;    // distance planes in LDS (else s.scratch)
   bool erode = false; // sg_erode_kernel (else the sweep kernel)
-  bool erode_wave = false;  // sg_erode_wave_kernel (one wave per env) when the map fits it
   size_t erode_lds = 0;
   int dist_nt = 256;
   bool grids_set = false;
@@ -1428,12 +1291,6 @@ int sg_ready(SgEnv* E, const char* who) {
 }
 
 hipError_t launch_dist(SgEnv* E, hipStream_t st) {
-  if (E->erode && E->erode_wave) {
-    const size_t lds = mcs::erode_wave_lds_bytes(E->s.W, E->s.L);
-    if (E->s.RW == 2) hipLaunchKernelGGL(mcs::sg_erode_wave_kernel<2>, dim3(E->s.B), dim3(64), lds, st, E->s);
-    else hipLaunchKernelGGL(mcs::sg_erode_wave_kernel<1>, dim3(E->s.B), dim3(64), lds, st, E->s);
-    return hipGetLastError();
-  }
   if (E->erode) {
     hipLaunchKernelGGL(mcs::sg_erode_kernel, dim3(E->s.B), dim3(256), E->erode_lds, st, E->s);
     return hipGetLastError();
@@ -1521,10 +1378,6 @@ int mc_sg_create(const mc_sg_config* cfg, int hip_device, void** out_env) {
     return v && atoi(v) == 1;
   }();
   E->erode = !force_sweep && c.width + c.length <= 257 && E->erode_lds <= mcs::kLdsLimit;
-  {  // MARLCOV_SG_ERODE_WAVE=0: the 4-wave erosion kernel (A/B; read per handle)
-    const char* ew = getenv("MARLCOV_SG_ERODE_WAVE");
-    E->erode_wave = E->erode && mcs::erode_wave_fits(c.width, c.length) && !(ew && atoi(ew) == 0);
-  }
   const int side = c.width > c.length ? c.width : c.length;
   E->dist_nt = side <= 64 ? 64 : (side <= 128 ? 128 : 256);
   const size_t B = s.B, N = s.N, G = s.G, mw = (size_t)s.W * s.RW;

@@ -117,18 +117,15 @@ BATCH_CASES = {
     "done_incr_small": (sg_cfg(numrobot=3, senseradius=2, done_thresh=0.3, done_incr=0.25, dist_reward=1),
                         (14, 14), 0.1, 10, 80),
     "r15_wide_window": (sg_cfg(numrobot=2, senseradius=15, free_penalty=0.05, dist_reward=1), (70, 90), 0.1, 4, 20),
-    # two row words per row in the one-wave erosion kernel (RW = 2; W = 128:
-    # every lane group holds four rows)
+    # two row words per row, W = 128 (the bench shape's rows), and an open grid
     "wave_rw2_128x124": (sg_cfg(numrobot=4, senseradius=2, free_penalty=0.1, dist_reward=1), (128, 124), 0.1, 6, 40),
     "wave_rw2_open_100x68": (sg_cfg(numrobot=3, senseradius=3, dist_reward=1), (100, 68), 0.0, 4, 40),
 }
 
 
-# the same cases with the one-lane-per-robot step kernel, with the whole
-# distance layer rewritten every step and with the 4-wave erosion kernel
-# instead of the one-wave kernel (all read when the handle is created)
-ALT_MODES = {"lane_per_robot": {"MARLCOV_SG_ROWS": "0"}, "full_dist_layer": {"MARLCOV_SG_FULL_DIST": "1"},
-             "erode_4wave": {"MARLCOV_SG_ERODE_WAVE": "0"}}
+# the same cases with the one-lane-per-robot step kernel and with the whole
+# distance layer rewritten every step (both read when the handle is created)
+ALT_MODES = {"lane_per_robot": {"MARLCOV_SG_ROWS": "0"}, "full_dist_layer": {"MARLCOV_SG_FULL_DIST": "1"}}
 ALT_CASES = ["n4_r2_dist", "scan_n6_r1_dist", "zero_cells_n3_r3", "n16_r2_dist", "done_incr_small",
              "wave_rw2_128x124"]
 

@@ -21,7 +21,7 @@ LIB = os.path.join(PKG, "libmarlcov_dstamps.so")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=8192)
-    ap.add_argument("--warmup", type=int, default=600)
+    ap.add_argument("--warmup", type=int, default=600)  # 5: the early phase after a reset
     ap.add_argument("--build-only", action="store_true")
     args = ap.parse_args()
     if args.build_only:
@@ -65,8 +65,12 @@ def main():
         if not m.any():
             print(f"  {name:22s} n=0")
             continue
+        # dist_fast_kernel's served maps: the try's staging, span + cell
+        # search, target search; the transform kernels: fast-path attempt, stage,
+        # strips, cache pass
+        labs = ("", "stage", "cells", "targets") if name == "fast path" else ("fast try", "stage", "strips", "cache")
         row = "  ".join(f"{lab} med {np.median(p[m]):8.0f} p90 {np.percentile(p[m], 90):8.0f} max {p[m].max():8d}"
-                        for lab, p in zip(("fast try", "stage", "strips", "cache"), ph))
+                        for lab, p in zip(labs, ph) if lab)
         print(f"  {name:22s} n={m.sum():5d}  {row}")
 
 
