@@ -186,6 +186,15 @@ __device__ __forceinline__ int tile_min_dist(uint64_t nb, int x0, int y0, int cx
   return cap;
 }
 
+// |c - the nearest set bit of row| (0 <= c < 64), or kInf for an empty row
+__device__ __forceinline__ int row_near(uint64_t row, int c) {
+  const uint64_t lo = row & ((2ull << c) - 1ull), hi = row >> c;  // (c = 63: 2 << 63 wraps to 0, lo = row)
+  int h = kInf;
+  if (lo) h = c - (63 - __clzll((unsigned long long)lo));
+  if (hi) h = min(h, __ffsll((unsigned long long)hi) - 1);
+  return h;
+}
+
 // max over the wave (every lane gets it)
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
@@ -230,8 +239,9 @@ __host__ __device__ inline DtLds dt_lds(int RX, int RY, int MT, int T) {
 // leaves the cells' new d in cdv, the targets' d in s_d (-1 stays: none),
 // the best (d << 16 | index) in *fkey and a target the 40 x 40 block cannot
 // settle in *ffail; `tried` = false when the box is too large to stage.
-// `span` (optional, 2 * kSpan words): the staged box's covered extent per
-// row and per column, for the cells outside the box's column or row band.
+// `span` (optional, 6 * kSpan words): the staged box's covered extent per
+// row and per column and their 1D transforms, for the cells outside the
+// box's column or row band.
 // Ends with a barrier.
 constexpr int kSpan = 256;  // box rows / columns the span arrays hold
 template <int NTH>
@@ -249,7 +259,7 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
   const int tx_c = (min(px - pad - 1, px - s.ego) + max(px - pad + 1, px + s.ego)) >> 1;
   const int ty_c = (min(py - pad - 1, py - s.ego) + max(py - pad + 1, py + s.ego)) >> 1;
   const int rti0 = (tx_c >> 3) - 2, rtj0 = (ty_c >> 3) - 2;
-  tried = nt + 25 <= kFastTiles;
+  tried = nt + 25 + 40 <= kFastTiles;  // the box, the 5 x 5 tiles, their 40 rows
   if (!tried) return;
   // the thread's cached cells (cell, d): loads in flight with the tiles'
   constexpr int KC = (kDistK + NTH - 1) / NTH;
@@ -260,7 +270,6 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     pcw[j] = k < ccnt ? cc[k] : 0;
     pcd[j] = k < ccnt ? cd[k] : 0;
   }
-  for (int t = tid; t < T; t += NTH) s_d[t] = kInf;
   for (int i = tid; i < nt + 25; i += NTH) {
     int ti, tj;
     if (i < nt) {
@@ -312,6 +321,24 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
       }
     }
     __syncthreads();
+    // the extents' 1D transforms: along the row axis (q = box row)
+    // tr[0][a] = min_q |a - q| + lo(q), tr[1][a] = min_q |a - q| - hi(q); the
+    // same along the column axis in tr[2], tr[3] (kInf: no covered cell)
+    int* tr = reinterpret_cast<int*>(span + 2 * kSpan);
+    const int nr = rspan ? NR : 0, nc = cspan ? NC : 0;
+    for (int i = tid; i < 2 * (nr + nc); i += NTH) {
+      const bool rows = i < 2 * nr;
+      const int k = rows ? i : i - 2 * nr, side = k & 1, a = k >> 1, n = rows ? nr : nc;
+      const uint32_t* sp = rows ? span : span + kSpan;
+      int best = kInf;
+      for (int q = 0; q < n; ++q) {
+        const uint32_t v = sp[q];
+        if ((v & 0xFFFFu) == 0xFFFFu) continue;
+        best = min(best, abs(a - q) + (side ? -(int)(v >> 16) : (int)(v & 0xFFFFu)));
+      }
+      tr[(rows ? 0 : 2 * kSpan) + side * kSpan + a] = best;
+    }
+    __syncthreads();
   }
   uint32_t mykey = 0;
 #pragma unroll
@@ -330,29 +357,16 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
     if (bdist < d && nt > 0 && ((rspan && gy > 0) || (cspan && gx > 0))) {
       // the cell is beside the box's column band (or row band): in every box
       // row the nearest covered cell is that row's first (last) covered
-      // column, so d = min over rows |cx - X| + the column gap; rows outward
-      // from the cell's, while the row distance alone stays below d
+      // column, so d = min over rows |cx - X| + the column gap, one read of
+      // the rows' 1D transform (a cell outside the row range: the nearest
+      // row's value plus the distance to it)
       const bool byrow = rspan && gy > 0 && (!(cspan && gx > 0) || NR <= NC);
       const int a = byrow ? cx - X0 : cy - Y0, n = byrow ? NR : NC;  // the cell along the span axis
       const int o = byrow ? cy - Y0 : cx - X0;                          // and across it (outside [0, n'))
-      const uint32_t* sp = byrow ? span : span + kSpan;
+      const int* tr = reinterpret_cast<const int*>(span + 2 * kSpan) + (byrow ? 0 : 2 * kSpan);
       const int ac = min(max(a, 0), n - 1);
-      for (int dr = 0; dr < n; ++dr) {
-        bool live = false;
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) {
-          const int q = sg ? ac + dr : ac - dr;
-          if ((sg && dr == 0) || q < 0 || q >= n) continue;
-          const int dq = abs(a - q);
-          if (dq + (byrow ? gy : gx) >= d) continue;
-          live = true;
-          const uint32_t v = sp[q];
-          if ((v & 0xFFFFu) != 0xFFFFu) d = min(d, dq + (o < 0 ? (int)(v & 0xFFFFu) - o : o - (int)(v >> 16)));
-        }
-        // both directions out of the span or the ball: the distance along
-        // the axis only grows from here
-        if (!live) break;
-      }
+      const int v = o < 0 ? tr[ac] : tr[kSpan + ac];
+      if (v < kInf / 2) d = min(d, abs(a - ac) + (o < 0 ? v - o : v + o));
     } else if (bdist < d && nt > 0) {
       const int ct = min(max(cx >> 3, ti0), ti1);  // the box tile row nearest the cell
       for (int dr = 0; dr <= nbr; ++dr) {
@@ -394,23 +408,34 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
       ty = py + (t == 2 ? 1 : (t == 4 ? -1 : 0)) - pad;
     }
   };
-  // d of each target: its 25 tiles as (target, tile) items over the threads
-  // (a thread per target walking 25 tiles was the try's latency chain), the
-  // minimum per target in LDS
-  for (int i = tid; i < 25 * T; i += NTH) {
-    const int t = i / 25, j = i - 25 * t, r = j / 5;
-    int tx, ty;
-    target_cell(t, tx, ty);
-    const int d = tile_min_dist(ft[nt + j], 8 * (rti0 + r), 8 * (rtj0 + j - 5 * r), tx, ty, kInf);
-    if (d < kInf) atomicMin(&s_d[t], d);
+  // the 40 x 40 block as row words (bit c: column 8 rtj0 + c)
+  uint64_t* brow = ft + nt + 25;
+  for (int r = tid; r < 40; r += NTH) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) w |= ((ft[nt + (r >> 3) * 5 + c] >> (8 * (r & 7))) & 0xFFull) << (8 * c);
+    brow[r] = w;
   }
   __syncthreads();
+  // d of each target: rows outward from its own while the row distance
+  // stays below the best d (a covered target, d = 0: one read); exact when
+  // d <= b, the distance to the block's outside, else the map is not served
   for (int t = tid; t < T; t += NTH) {
     int tx, ty;
     target_cell(t, tx, ty);
-    // exact only if no cell outside the 40 x 40 block can be nearer
-    const int b = min(min(tx - 8 * rti0, 8 * rti0 + 39 - tx), min(ty - 8 * rtj0, 8 * rtj0 + 39 - ty)) + 1;
-    if (s_d[t] > b) *ffail = 1;
+    const int lx = tx - 8 * rti0, ly = ty - 8 * rtj0;
+    const int b = min(min(lx, 39 - lx), min(ly, 39 - ly)) + 1;
+    int d = b + 1;
+    if (b > 0) {
+      d = min(d, row_near(brow[lx], ly));
+      for (int dr = 1; dr < d; ++dr) {
+        const int up = lx - dr >= 0 ? row_near(brow[lx - dr], ly) : kInf;
+        const int dn = lx + dr < 40 ? row_near(brow[lx + dr], ly) : kInf;
+        d = min(d, dr + min(up, dn));
+      }
+    }
+    if (d > b) *ffail = 1;
+    else s_d[t] = d;
   }
   __syncthreads();
 }
@@ -576,7 +601,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       // ---- merge the parts' partials: the best key, the raw target d (in
       // the output buffers), the strip maxima, the cache candidates
       __syncthreads();  // the item's LDS scalars are initialised
-      const uint32_t total = s.dist_gcnt[ea];  // every part published its candidates
+      // the parts' candidates: a one-pass list (with theta0), else none
+      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
       const unsigned long long gk = s.dist_gkey[ea];
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
       for (int t = tid; t < T; t += kDtThreads)
@@ -603,7 +629,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s.dist_gcnt[ea] = 0;
       }
       __syncthreads();
-      need_cb = s_cov && s_ccount > kDistK;  // an overflowed list: the second pass
+      need_cb = s_cov && !(kOnePass && theta0 > 0 && s_ccount <= kDistK);  // the second pass
     }
     if (!fast && need_cb) {
       if (mode != 3)  // (mode 3 holds the parts' targets)
@@ -940,25 +966,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
         if ((ran >> st) & 1ull) s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
-      if (!(kOnePass && theta0 > 0) && s.dist_ch && nstrips > 0) {
-        // no one-pass list (no theta0): the part's own cache candidates in a
-        // second pass over its strips, from the best lower bound of the new
-        // max at hand -- its own max, or the global key so far (any value
-        // read is a max of exact maxima)
-        const unsigned long long gk = __hip_atomic_load(s.dist_gkey + ea, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int thr = max((int)(s_key >> 48), (int)(gk >> 48)) - kDistT;
-        if (thr >= 0) {
-          carry_in(st_lo);
-          for (int st = st_lo; st < st_hi; ++st) {
-            if (st >= kMaxTrack || s_smax[st] >= thr) strip(st, thr, -1);
-            else carry_over(st);
-          }
-        } else if (tid == 0) {
-          s_ccount = kDistK + 1;  // no useful bound: mode 3's second pass
-        }
-        __syncthreads();
-      }
-      if (s.dist_ch) {
+      if (kOnePass && theta0 > 0) {
         const int n = s_ccount;
         if (n > 0) {
           if (tid == 0) s_base = atomicAdd(s.dist_gcnt + ea, (uint32_t)(n <= kDistK ? n : kGCand + 1));
@@ -989,7 +997,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         // reaches it; the others only carry their last covered column)
         int cnt = -1;
         // the main pass's list (mode 3: the parts' lists) holds them all
-        const bool main_ok = (mode == 3 || (kOnePass && theta0 > 0)) && s_ccount <= kDistK;
+        const bool main_ok = kOnePass && theta0 > 0 && s_ccount <= kDistK;
         if (cov && M >= 0 && main_ok) {
           const int thr = M - kDistT, n = s_ccount;
           for (int k = tid; k < n; k += kDtThreads)
@@ -1009,8 +1017,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           const int thr = M - kDistT;
           carry_in(0);
           for (int st = 0; st < nstrips_all; ++st) {
-            if (st >= kMaxTrack || s_smax[st] >= thr) strip(st, thr, -1);
-            else carry_over(st);
+            if (st >= kMaxTrack || s_smax[st] >= thr) {
+              strip(st, thr, -1);
+              __syncthreads();
+              if (s_ccount > kDistK) break;  // overflowed: no cache for this map, the rest is moot
+            } else {
+              carry_over(st);
+            }
           }
           __syncthreads();
           cnt = s_ccount <= kDistK ? s_ccount : -1;
@@ -1119,7 +1132,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   __shared__ uint32_t s_served, s_nf, s_fbase, s_nc;
   __shared__ uint2 s_fl[kFastBuf];     // this workgroup's maps for the full list
   __shared__ uint32_t s_cl[kFastBuf];  // this chunk's maps with a cache
-  __shared__ uint32_t s_span[2 * kSpan];
+  __shared__ uint32_t s_span[6 * kSpan];
   const int tid = threadIdx.x;
   const int T = 5 + s.E * s.E;
   const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
