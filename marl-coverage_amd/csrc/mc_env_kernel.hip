@@ -1610,10 +1610,11 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
 template <int NT, class SH>
 constexpr int env_min_waves() {
 #ifdef MC_C4_WPE
-  return (NT == 256 && SH::NB == 360) ? MC_C4_WPE : 1;
-#else
-  return 1;
+  if (NT == 256 && SH::NB == 360) return MC_C4_WPE;
 #endif
+  // C5 (16 agents): the robots in registers for the moves and the obs crops
+  // would take the kernel past 128 VGPRs (3 waves per SIMD); keep 4
+  return SH::N == 16 ? 4 : 1;
 }
 
 template <int NT, int EPW, typename WT, class SH>
@@ -1796,6 +1797,8 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     if constexpr (!FRONT && !EARLY) {  // (FRONT, EARLY: moved during round trip 2)
       // the first wave of the slot moves the robots (lane 0 publishes); the
       // other waves of a multi-wave workgroup only wait at the barrier
+      // (moves_regs for 16 agents, C5: 17.7k vs 7.3k cycles per wave -- the
+      // every-lane replay of 256 position compares outweighs the broadcasts)
       if constexpr (SH::N > 0 && SH::N <= 8) {
         if (NT == 64 || C.sub < 64) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
       } else if (C.sub < 64) {
@@ -1804,6 +1807,20 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       __syncthreads();
     }
     STAMP(3);
+    // dist_reward: lane i < N loads its agent's PRE terms (the last step's
+    // dist kernels wrote them) now that its move is known; they land during
+    // the sensing
+    // (compiled shapes; the generic kernels keep the loads in the reward:
+    // two more live registers there cost the u64 ones a wave per SIMD)
+    constexpr bool kPrePrefetch = SH::N > 0;
+    float dpre0 = 0.0f, dprek = 0.0f;
+    if (kPrePrefetch && s.dist && C.sub < N) {
+      const int dx = L.x[C.sub] - L.x0[C.sub], dy = L.y[C.sub] - L.y0[C.sub];
+      const int k = dx == 1 ? 1 : (dy == 1 ? 2 : (dx == -1 ? 3 : (dy == -1 ? 4 : 0)));
+      const float* pr = s.dist_pre + ((size_t)e * N + C.sub) * 8;
+      dpre0 = pr[0];
+      dprek = pr[1 + k];
+    }
     sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM>(s, C, I);
     __syncthreads();
     STAMP(5);
@@ -1817,13 +1834,21 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       const int cs = currstep0 + 1;                          // :154
       // observe() :206-258 returns the float32 sum of the agents' distance
       // terms (dist_reward, agent order) plus the union delta (float64)
+      // (only lane 0's value is stored: the agents' terms are in the slot's
+      // first lanes, N <= 64, and are summed in agent order)
       float dsum = 0.0f;
       if (s.dist) {
-        for (int i = 0; i < N; ++i) {
-          const int dx = L.x[i] - L.x0[i], dy = L.y[i] - L.y0[i];
-          const int k = dx == 1 ? 1 : (dy == 1 ? 2 : (dx == -1 ? 3 : (dy == -1 ? 4 : 0)));
-          const float* pr = s.dist_pre + ((size_t)e * N + i) * 8;
-          dsum = __fadd_rn(dsum, dist_value(pr[1 + k], pr[0]));  // :222-223,239-240
+        if constexpr (kPrePrefetch) {
+          const float term = dist_value(dprek, dpre0);  // :222-223,239-240
+          for (int i = 0; i < N; ++i)
+            dsum = __fadd_rn(dsum, __builtin_bit_cast(float, bcast(C, __builtin_bit_cast(int, term), i)));
+        } else {
+          for (int i = 0; i < N; ++i) {
+            const int dx = L.x[i] - L.x0[i], dy = L.y[i] - L.y0[i];
+            const int k = dx == 1 ? 1 : (dy == 1 ? 2 : (dx == -1 ? 3 : (dy == -1 ? 4 : 0)));
+            const float* pr = s.dist_pre + ((size_t)e * N + i) * 8;
+            dsum = __fadd_rn(dsum, dist_value(pr[1 + k], pr[0]));  // :222-223,239-240
+          }
         }
       }
       const double obs_reward = (double)dsum + (double)c->cnt_vis;
@@ -1950,7 +1975,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
                 ObsFast<SH::EGO, SH::N, SH::LC>::NB <= CtxT::LPE) {
     write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the wave
   } else {
-    if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 8) ? SH::N : 0>(s, C, obs_out);
+    if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 16) ? SH::N : 0>(s, C, obs_out);
   }
   STAMP(9);
   if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
