@@ -28,11 +28,13 @@ def main():
         "steps": s["steps"],
         "hbm_bytes_per_launch": total,
         "per_kernel": {k: {"hbm_bytes": v.get("hbm_bytes"), "read": v.get("hbm_read_bytes"),
-                           "write": v.get("hbm_write_bytes"), "mean_us": v["mean_us"]} for k, v in ks.items()},
-        "step_mean_us": round(sum(v["mean_us"] for v in ks.values()), 3),
+                           "write": v.get("hbm_write_bytes"), "mean_us": v["mean_us"],
+                           "dispatches_per_step": v.get("dispatches_per_step", 1),
+                           "per_step_us": v.get("per_step_us", v["mean_us"])} for k, v in ks.items()},
+        "step_mean_us": round(sum(v.get("per_step_us", v["mean_us"]) for v in ks.values()), 3),
         "source": f"tools/prof_config.py --config {s['config']} --steps {s['steps']} --warmup {s['warmup']}: "
-                  "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, last `steps` dispatches of each "
-                  "per-step kernel (the timed region), FETCH_SIZE x2 (gfx950 counts half of each 128-B request)",
+                  "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, the timed region's dispatches of each "
+                  "per-step kernel (bytes per step), FETCH_SIZE x2 (gfx950 counts half of each 128-B request)",
     }
     dst = os.path.join(ROOT, "profiles", f"traffic_{s['config']}.json")
     with open(dst, "w") as f:
