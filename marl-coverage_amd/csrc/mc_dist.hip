@@ -1284,9 +1284,13 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
                      pre_out, dist_obs, list, count, full);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, 2048, 2, full, stream);
+  // grids of about the resident workgroups (two per CU); mode 2 has at most
+  // kSplitSlots items when it splits (a 2048-workgroup grid measured the
+  // same: 202.3 vs 202.3 us per C5 steady step, profiles/r4/c5_grid/)
+  const unsigned g2 = (unsigned)(maps < (size_t)kSplitSlots ? maps : (size_t)kSplitSlots);
+  e = launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, g2, 2, full, stream);
   if (e != hipSuccess) return e;
-  return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, grid < 1024 ? grid : 1024, 3, full, stream);
+  return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, g2 < 256 ? g2 : 256, 3, full, stream);
 }
 
 }  // namespace mc

@@ -1797,8 +1797,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     if constexpr (!FRONT && !EARLY) {  // (FRONT, EARLY: moved during round trip 2)
       // the first wave of the slot moves the robots (lane 0 publishes); the
       // other waves of a multi-wave workgroup only wait at the barrier
-      // (moves_regs for 16 agents, C5: 17.7k vs 7.3k cycles per wave -- the
-      // every-lane replay of 256 position compares outweighs the broadcasts)
+      // (C5, 16 agents: moves_regs took 17.7k vs 7.3k cycles per wave -- the
+      // every-lane replay of 256 position compares outweighs the broadcasts;
+      // the loop on the scalar unit from v_readlane copies, 111.3 vs 107.8 us
+      // per env kernel, profiles/r4/c5_grid/)
       if constexpr (SH::N > 0 && SH::N <= 8) {
         if (NT == 64 || C.sub < 64) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
       } else if (C.sub < 64) {
