@@ -481,7 +481,10 @@ __device__ __forceinline__ void cache_serve(const State& s, int T, uint32_t ea, 
 //      stores before the merge: no per-map done counter, no device-scope
 //      fences between the XCDs' L2s
 constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
-constexpr int kMaxParts = 8;
+#ifndef MC_MAX_PARTS  // build knob (A/B): parts per split map
+#define MC_MAX_PARTS 8
+#endif
+constexpr int kMaxParts = MC_MAX_PARTS;
 constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
 
 template <int kCL>
@@ -635,38 +638,44 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (mode != 3)  // (mode 3 holds the parts' targets)
         for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
       {
-        // the agent's tiles (coalesced loads) scattered as row bytes into map
-        // rows in the strip area (free until the strips start): byte tj of map
-        // row X = row X & 7 of tile (X >> 3, tj); the bytes past the last tile
-        // column are zeroed by their row's thread.  Then the extended rows:
-        // map columns shifted right by pad (a funnel shift of two words)
+        // the agent's tiles as map rows in the strip area (free until the
+        // strips start): a thread takes 8 tiles of one tile row (one 64-column
+        // word of 8 map rows), loads them, and transposes their bytes with
+        // v_perm -- byte j of row word r = byte r of tile j -- into 8 word
+        // stores (was 64 byte stores per 8 tiles).  Tiles past the last tile
+        // column load as 0.  Then the extended rows: map columns shifted
+        // right by pad (a funnel shift of two words)
         uint8_t* crow = reinterpret_cast<uint8_t*>(G);
+        uint64_t* crw = reinterpret_cast<uint64_t*>(G);
         const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
-        const int RB = RWm * 8;           // bytes per map row
-        // eight tiles' loads in flight per thread, then their bytes; the
-        // block row of tile i by a magic reciprocal (no division)
-        const uint32_t mT = magic_div((uint32_t)s.TCS);
-        for (int i0 = tid; i0 < s.MT; i0 += 8 * kDtThreads) {
-          uint64_t tv[8];
+        for (int q = tid; q < s.TR * RWm; q += kDtThreads) {
+          const int ti = q / RWm, w = q - ti * RWm;
+          uint32_t lo[8], hi[8];  // tile j's dwords (rows 0-3, rows 4-7)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int i = i0 + k * kDtThreads;
-            tv[k] = i < s.MT ? free_t[i] : 0ull;
+          for (int j = 0; j < 8; ++j) {
+            const int tj = 8 * w + j;
+            const uint64_t t = tj < s.TC ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
+            lo[j] = (uint32_t)t;
+            hi[j] = (uint32_t)(t >> 32);
           }
+          const int nr = min(8, s.Wp - 8 * ti);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int i = i0 + k * kDtThreads;
-            const int blk = i >> 4, bi = mT ? (int)__umulhi((uint32_t)blk, mT) : blk, bj = blk - bi * s.TCS;
-            const int ti = 4 * bi + ((i >> 2) & 3), tj = 4 * bj + (i & 3);
-            if (i < s.MT && ti < s.TR && tj < s.TC) {
-#pragma unroll
-              for (int r = 0; r < 8; ++r)
-                if (8 * ti + r < s.Wp) crow[(size_t)(8 * ti + r) * RB + tj] = (uint8_t)(tv[k] >> (8 * r));
-            }
+          for (int r = 0; r < 8; ++r) {
+            if (r >= nr) break;
+            const uint32_t* src = r < 4 ? lo : hi;
+            const uint32_t b = (uint32_t)(r & 3);
+            // byte b of src[j]: pairs (j, j + 1) -> bytes 0, 1 of a dword,
+            // then two such pairs -> 4 bytes
+            const uint32_t sel2 = b | ((4u + b) << 8) | 0x0C0C0000u;
+            const uint32_t p01 = __builtin_amdgcn_perm(src[1], src[0], sel2);
+            const uint32_t p23 = __builtin_amdgcn_perm(src[3], src[2], sel2);
+            const uint32_t p45 = __builtin_amdgcn_perm(src[5], src[4], sel2);
+            const uint32_t p67 = __builtin_amdgcn_perm(src[7], src[6], sel2);
+            const uint32_t wlo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+            const uint32_t whi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
+            crw[(size_t)(8 * ti + r) * RWm + w] = (uint64_t)wlo | ((uint64_t)whi << 32);
           }
         }
-        for (int X = tid; X < s.Wp; X += kDtThreads)
-          for (int b = s.TC; b < RB; ++b) crow[(size_t)X * RB + b] = 0;
         __syncthreads();
         const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
         int any = 0;
@@ -978,6 +987,19 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                 s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
         }
       }
+#ifdef MC_DIST_STAMPS
+      {  // a part (flag bit 52): stage, strips, publish (mode 3 leaves these)
+        uint64_t tp = 0;
+        DSTAMP(tp);
+        if (tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u) {
+          auto f16 = [](uint64_t a, uint64_t b) -> uint64_t {
+            const uint64_t d = (b - a) >> 4;
+            return d < 0xFFFFull ? d : 0xFFFFull;
+          };
+          s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, tp) << 32) | (1ull << 52);
+        }
+      }
+#endif
       __syncthreads();  // the LDS is reused by the next item
       continue;
     }
@@ -1055,7 +1077,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     }
     DSTAMP(ts3);
 #ifdef MC_DIST_STAMPS
-    if (tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u) {
+    if (tid == 0 && s.stamps && ea < (uint32_t)s.B * 16u && mode != 3) {
       auto f16 = [](uint64_t a, uint64_t b) -> uint64_t {
         const uint64_t d = (b - a) >> 4;
         return d < 0xFFFFull ? d : 0xFFFFull;

@@ -59,7 +59,9 @@ def main():
     second = (s >> np.uint64(50)) & np.uint64(1)
     ph = [((s >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
     ph.insert(0, (s >> np.uint64(51)).astype(np.int64) * 64)  # the fast-path attempt (part of stage)
-    for name, m in (("fast path", fast == 1), ("full, one-pass list", (fast == 0) & (kept == 1)),
+    part = (s >> np.uint64(52)) & np.uint64(1)  # a split map's part (mode 2; mode 3 does not stamp)
+    fast = fast & (np.uint64(1) - part)
+    for name, m in (("split part", part == 1), ("fast path", fast == 1), ("full, one-pass list", (fast == 0) & (kept == 1)),
                     ("full, second pass", (fast == 0) & (second == 1)),
                     ("full, no cache", (fast == 0) & (kept == 0) & (second == 0))):
         if not m.any():
@@ -68,7 +70,8 @@ def main():
         # dist_fast_kernel's served maps: the try's staging, span + cell
         # search, target search; the transform kernels: fast-path attempt, stage,
         # strips, cache pass
-        labs = ("", "stage", "cells", "targets") if name == "fast path" else ("fast try", "stage", "strips", "cache")
+        labs = (("", "stage", "cells", "targets") if name == "fast path" else
+                ("", "stage", "strips", "publish") if name == "split part" else ("fast try", "stage", "strips", "cache"))
         row = "  ".join(f"{lab} med {np.median(p[m]):8.0f} p90 {np.percentile(p[m], 90):8.0f} max {p[m].max():8d}"
                         for lab, p in zip(labs, ph) if lab)
         print(f"  {name:22s} n={m.sum():5d}  {row}")
