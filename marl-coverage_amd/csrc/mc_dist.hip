@@ -529,11 +529,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   const bool strided = mode >= 2 || list != nullptr;
   if (mode == 2 && blockIdx.x == 0 && tid == 0) {
     // mode 1 has drained the list: its counters for the diagnostics
-    // (MC_FIELD_DIST_LISTED / _CACHED) and empty for the next step's env
+    // (MC_FIELD_DIST_LISTED / _CACHED: every listed map was either served by
+    // the cache or put on the full list -- no served-count atomic per
+    // workgroup, all on one address) and empty for the next step's env
     // kernel (no per-workgroup done counters in modes 1 / 2; the env kernel
     // empties the full list)
     count[2] = count[0];
-    count[4] = count[3];
+    count[4] = count[0] - nF;
     count[0] = 0;
     count[3] = 0;
   }
@@ -1151,7 +1153,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   __shared__ uint16_t cdv[kDistK];
   __shared__ uint32_t s_fkey;
   __shared__ int s_ffail;
-  __shared__ uint32_t s_served, s_nf, s_fbase, s_nc;
+  __shared__ uint32_t s_nf, s_fbase, s_nc;
   __shared__ uint2 s_fl[kFastBuf];     // this workgroup's maps for the full list
   __shared__ uint32_t s_cl[kFastBuf];  // this chunk's maps with a cache
   __shared__ uint32_t s_span[6 * kSpan];
@@ -1160,7 +1162,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
   uint64_t tk0 = 0;
   DSTAMP(tk0);
-  if (tid == 0) s_served = s_nf = 0;
+  if (tid == 0) s_nf = 0;
   // a contiguous share of the list per workgroup, kFastBuf maps at a time:
   // one thread per map reads its cache header (a map without a cache goes
   // straight to the full list), then the workgroup tries the cache of each
@@ -1212,7 +1214,6 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
       const bool served = tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
       if (served) {
         cache_serve<kFastThreads>(s, T, ea, s_fkey, ccnt, cM0, cdv, s_dyn, pre_out, dist_obs, nullptr);
-        if (tid == 0) ++s_served;
       } else if (tid == 0) {
         to_full(ea, tried ? (s_fkey >> 16) : 0u);
       }
@@ -1237,11 +1238,9 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
     }
   }
   if (tid == 0 && s_nf > (uint32_t)kFastBuf) s_nf = kFastBuf;  // the rest went to the list directly
-  // one atomic per workgroup for the served count and for the full list
-  if (tid == 0) {
-    if (s_served) atomicAdd(count + 3, s_served);  // MC_FIELD_DIST_CACHED
-    s_fbase = s_nf ? atomicAdd(full, s_nf) : 0u;
-  }
+  // one atomic per workgroup for the full list (the served count follows
+  // from the list lengths, mode 2)
+  if (tid == 0) s_fbase = s_nf ? atomicAdd(full, s_nf) : 0u;
   __syncthreads();
   for (uint32_t k = tid; k < s_nf; k += kFastThreads) reinterpret_cast<uint2*>(full + 8)[s_fbase + k] = s_fl[k];
 }
