@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 7
+#define MARLCOV_ABI_VERSION 8
 
 enum {
   MC_OK = 0,
@@ -149,7 +149,12 @@ enum {
   MC_FIELD_DIST_CACHED = 19, /* int32 [1] of the maps the last POST listed, those
                                 the top-cell cache served without a full
                                 transform (read-only diagnostic)               */
-  MC_FIELD_COUNT = 20
+  MC_FIELD_DIST_TOTALS = 20, /* uint64 [4] cumulative since mc_create: maps the
+                                POSTs listed, of them served by the top-cell
+                                cache, fully transformed, and POST launches
+                                (read-only diagnostic: a caller takes deltas;
+                                the bench's C5 design bytes)    */
+  MC_FIELD_COUNT = 21
 };
 
 int32_t mc_abi_version(void);
@@ -222,7 +227,11 @@ int mc_step(void* env, const uint8_t* dev_actions, double* dev_reward,
  * dijkstra launches of the config), stream-ordered.  For callers whose
  * actions are known ahead (open-loop rollouts, benchmarks): one FFI crossing
  * instead of num_steps.  Same semantics as the reference's step
- * (dec_grid_rl.py:91-169) applied num_steps times. */
+ * (dec_grid_rl.py:91-169) applied num_steps times.  Strides are in bytes
+ * (0: every step writes the same buffer); reward_stride must be a multiple of
+ * 8.  Arguments are checked before anything is enqueued; if a launch of step
+ * k fails, steps 0..k-1 are already enqueued (the env has advanced k steps)
+ * and mc_last_error() names k. */
 int mc_step_many(void* env, const uint8_t* dev_actions, int64_t actions_stride, int32_t num_steps,
                  double* dev_reward, int64_t reward_stride, uint8_t* dev_done, int64_t done_stride,
                  void* dev_obs, int64_t obs_stride, uint8_t* dev_adj, int64_t adj_stride,

@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
@@ -21,7 +21,7 @@ ACT_NOOP = 4
 (FIELD_POS, FIELD_MOVED, FIELD_FREE, FIELD_OBST, FIELD_VISITED, FIELD_FREE_COUNT,
  FIELD_VISITED_COUNT, FIELD_CURRSTEP, FIELD_DONE_THRESH, FIELD_ENV_GRID, FIELD_EPISODE,
  FIELD_NUMFREE, FIELD_GRID_NEG, FIELD_GRID_POS, FIELD_DIST_MW, FIELD_DIST_LISTED, FIELD_EP_PC,
- FIELD_EP_LEN, FIELD_DJ_LISTED, FIELD_DIST_CACHED) = range(20)
+ FIELD_EP_LEN, FIELD_DJ_LISTED, FIELD_DIST_CACHED, FIELD_DIST_TOTALS) = range(21)
 
 
 class McConfig(ctypes.Structure):

@@ -26,7 +26,7 @@ _FIELD_DTYPES = {
     _lib.FIELD_NUMFREE: "int32", _lib.FIELD_GRID_NEG: "int64", _lib.FIELD_GRID_POS: "int64",
     _lib.FIELD_DIST_MW: "int32", _lib.FIELD_DIST_LISTED: "int32",
     _lib.FIELD_EP_PC: "float64", _lib.FIELD_EP_LEN: "int32", _lib.FIELD_DJ_LISTED: "int32",
-    _lib.FIELD_DIST_CACHED: "int32",
+    _lib.FIELD_DIST_CACHED: "int32", _lib.FIELD_DIST_TOTALS: "int64",
 }
 
 
@@ -260,9 +260,16 @@ class BatchCoverageEnv:
         """Step K times with known actions, one C-ABI call (mc_step_many):
         ``actions`` uint8 [K, B, N] device tensor; returns new tensors obs
         [K, B, N, Lc, E, E], reward [K, B], done [K, B] -- step k's outputs,
-        exactly what K ``step`` calls would have returned.  (The adjacency
-        and the float dist / minimap layers keep only the last step's.)"""
+        exactly what K ``step`` calls would have returned, with the per-step
+        adjacency [K, B, N, N] as ``((obs, adj), reward, done)`` when the env
+        returns it.  Configs with float obs layers (dist_reward, minimap) keep
+        one registered float buffer per env (mc_set_dist_obs /
+        mc_set_minimap_obs), so their per-step float layers cannot come back
+        from one call: use ``step`` for them."""
         torch = self._torch
+        if self.dist_obs is not None or self.minimap_obs is not None:
+            raise ValueError("rollout: dist_reward / mini_map_rad configs write their float obs layers to one "
+                             "registered buffer; step() returns them per step")
         a = actions
         if not (isinstance(a, torch.Tensor) and a.dtype == torch.uint8 and a.device == self.device
                 and a.is_contiguous()):
@@ -273,14 +280,22 @@ class BatchCoverageEnv:
         obs = torch.empty((K,) + tuple(self.obs.shape), dtype=torch.uint8, device=self.device)
         rew = torch.empty((K, self.num_envs), dtype=torch.float64, device=self.device)
         done = torch.empty((K, self.num_envs), dtype=torch.uint8, device=self.device)
-        if K == 0:
-            return obs, rew, done
-        _lib.check(self.lib.mc_step_many(self._h, a.data_ptr(), a[0].numel(), K, rew.data_ptr(), rew[0].numel() * 8,
-                                         done.data_ptr(), done[0].numel(), obs.data_ptr(), obs[0].numel(),
-                                         self._adj_ptr(), 0, self._stream()), "mc_step_many")
-        self.obs.copy_(obs[-1])
-        self.reward.copy_(rew[-1])
-        self.done.copy_(done[-1])
+        adj = None
+        if self.adj is not None:
+            adj = torch.empty((K,) + tuple(self.adj.shape), dtype=self.adj.dtype, device=self.device)
+        if K > 0:
+            _lib.check(self.lib.mc_step_many(self._h, a.data_ptr(), a[0].numel(), K, rew.data_ptr(),
+                                             rew[0].numel() * 8, done.data_ptr(), done[0].numel(), obs.data_ptr(),
+                                             obs[0].numel(), adj.data_ptr() if adj is not None else None,
+                                             adj[0].numel() if adj is not None else 0, self._stream()),
+                       "mc_step_many")
+            self.obs.copy_(obs[-1])
+            self.reward.copy_(rew[-1])
+            self.done.copy_(done[-1])
+            if adj is not None:
+                self.adj.copy_(adj[-1])
+        if adj is not None:
+            return (obs, adj), rew, done
         return obs, rew, done
 
     def step_many_raw(self, actions_ptr: int, actions_stride: int, num_steps: int, reward_ptr: int,
@@ -322,7 +337,7 @@ class BatchCoverageEnv:
             _lib.FIELD_GRID_NEG: (G,) + mw, _lib.FIELD_GRID_POS: (G,) + mw,
             _lib.FIELD_DIST_MW: (B, N, 2), _lib.FIELD_DIST_LISTED: (1,),
             _lib.FIELD_EP_PC: (B,), _lib.FIELD_EP_LEN: (B,), _lib.FIELD_DJ_LISTED: (1,),
-            _lib.FIELD_DIST_CACHED: (1,),
+            _lib.FIELD_DIST_CACHED: (1,), _lib.FIELD_DIST_TOTALS: (4,),
         }[field]
 
     def get_state(self, field, out=None):

@@ -119,6 +119,7 @@ FieldDesc field(Env* E, int f) {
     case MC_FIELD_EP_PC: return {s.ep_pc, B * 8};
     case MC_FIELD_EP_LEN: return {s.ep_len, B * 4};
     case MC_FIELD_DJ_LISTED: return {E->dj_list ? E->dj_list + 2 : nullptr, E->dj_list ? 4 : -1};
+    case MC_FIELD_DIST_TOTALS: return {s.dist_tot, s.dist_tot ? 32 : -1};
     default: return {nullptr, -1};
   }
 }
@@ -145,6 +146,18 @@ int env_threads(const mc::State& s) {
 }
 
 Env* as_env(void* p) { return static_cast<Env*>(p); }
+
+// lanes per env workgroup and envs per workgroup for the current state
+// (mc_create, and again when mc_set_beam_table changes the beam count)
+void set_launch_shape(Env* E) {
+  E->nt = env_threads(E->s);
+  if (const char* ov = getenv("MARLCOV_NT")) {  // tuning / test override (64..1024)
+    const int v = atoi(ov);
+    if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) E->nt = v > E->nt ? v : E->nt;
+  }
+  E->epw = mc::env_pack(E->s);
+  if (E->nt > 64) E->epw = 1;  // (only the MARLCOV_NT override gets here with a packable env)
+}
 
 // envs per workgroup for this launch; MARLCOV_EPW=1 forces one env per
 // workgroup (A/B tuning)
@@ -331,12 +344,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       return fail(MC_EHIP, "mc_create: initial upload failed");
     }
   }
-  E->nt = env_threads(s);
-  if (const char* ov = getenv("MARLCOV_NT")) {  // tuning override (64..1024)
-    const int v = atoi(ov);
-    if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) E->nt = v > E->nt ? v : E->nt;
-  }
-  E->epw = mc::env_pack(s);
+  set_launch_shape(E);
   if (c.dijkstra_input) {
     // the BFS bitboards of one (env, agent) live in one workgroup's LDS
     const size_t need = mc::dijkstra_lds_bytes(s, c.pad);
@@ -394,9 +402,9 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->s.dist_pre = E->dist_pre;
     // (M, witness) per map, M = -1 (unknown) until a full transform; the
     // work list of the full transform and its count
-    void *mw = nullptr, *lq = nullptr;
+    void *mw = nullptr, *lq = nullptr, *tq = nullptr;
     if (dev_alloc(E, &mw, (size_t)s.B * s.N * 8) != MC_OK ||
-        dev_alloc(E, &lq, ((size_t)s.B * s.N + 5) * 4) != MC_OK ||
+        dev_alloc(E, &lq, ((size_t)s.B * s.N + 5) * 4) != MC_OK || dev_alloc(E, &tq, 32) != MC_OK ||
         hipMemset(mw, 0xFF, (size_t)s.B * s.N * 8) != hipSuccess) {
       std::string msg = g_err;
       mc_destroy(E);
@@ -405,6 +413,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->s.dist_mw = (int32_t*)mw;
     E->dist_list = (uint32_t*)lq;
     E->s.dist_cnt = E->dist_list;
+    E->s.dist_tot = (unsigned long long*)tq;
     // the top-cell cache (mc_dist.hip), off with map sharing (other agents'
     // maps add cells outside the agent's own sensing windows) or
     // MARLCOV_DIST_CACHE=0
@@ -722,8 +731,7 @@ int mc_set_beam_table(void* env, const double* host_table, int32_t num_beams) {
     E->s.nbeams = num_beams;
     E->s.mg_nb = mc::magic_div((uint32_t)num_beams);
     E->cfg.num_beams = num_beams;
-    E->nt = env_threads(E->s);
-    E->epw = mc::env_pack(E->s);
+    set_launch_shape(E);
   }
   HIP_TRY(hipMemcpy((void*)E->s.beams, bt.data(), (size_t)num_beams * sizeof(mc::Beam),
                     hipMemcpyHostToDevice));
@@ -934,6 +942,7 @@ int mc_step_many(void* env, const uint8_t* dev_actions, int64_t actions_stride, 
   if (num_steps < 0 || actions_stride < 0 || reward_stride < 0 || done_stride < 0 || obs_stride < 0 ||
       adj_stride < 0)
     return fail(MC_EINVAL, "mc_step_many: negative step count or stride");
+  if (reward_stride % 8 != 0) return fail(MC_EINVAL, "mc_step_many: reward_stride must be a multiple of 8 bytes");
   int rc = ready(E, "mc_step_many");
   if (rc) return rc;
   HIP_TRY(hipSetDevice(E->device));
@@ -943,7 +952,11 @@ int mc_step_many(void* env, const uint8_t* dev_actions, int64_t actions_stride, 
                    reinterpret_cast<double*>(reinterpret_cast<char*>(dev_reward) + k * reward_stride),
                    dev_done + k * done_stride, static_cast<char*>(dev_obs) + k * obs_stride,
                    dev_adj ? dev_adj + k * adj_stride : nullptr, st);
-    if (rc) return rc;
+    if (rc) {  // steps 0..k-1 are enqueued: the env has advanced k steps
+      std::string msg = g_err;
+      return fail(rc, "mc_step_many: step %d of %d failed after %d steps were enqueued: %s", (int)k,
+                  (int)num_steps, (int)k, msg.c_str());
+    }
   }
   return MC_OK;
 }
@@ -973,7 +986,7 @@ int mc_set_state(void* env, int32_t f, const void* dev_src, int64_t bytes, void*
   FieldDesc d = field(E, f);
   if (!d.ptr) return fail(MC_EINVAL, "unknown state field %d", f);
   if (f == MC_FIELD_DIST_MW || f == MC_FIELD_DIST_LISTED || f == MC_FIELD_EP_PC || f == MC_FIELD_EP_LEN ||
-      f == MC_FIELD_DJ_LISTED || f == MC_FIELD_DIST_CACHED)
+      f == MC_FIELD_DJ_LISTED || f == MC_FIELD_DIST_CACHED || f == MC_FIELD_DIST_TOTALS)
     return fail(MC_EINVAL, "field %d is derived state (read-only)", f);
   if (bytes != d.bytes) return fail(MC_EINVAL, "field %d is %lld bytes, got %lld", f, (long long)d.bytes, (long long)bytes);
   HIP_TRY(hipSetDevice(E->device));

@@ -536,6 +536,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // empties the full list)
     count[2] = count[0];
     count[4] = count[0] - nF;
+    if (s.dist_tot) {  // MC_FIELD_DIST_TOTALS (one thread, stream-ordered)
+      s.dist_tot[0] += count[0];
+      s.dist_tot[1] += count[0] - nF;
+      s.dist_tot[2] += nF;
+      s.dist_tot[3] += 1ull;
+    }
     count[0] = 0;
     count[3] = 0;
   }
@@ -1101,13 +1107,23 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   if (list && threadIdx.x == 0) {
     uint32_t* cnt = count;
     if (n_items == 0) {
-      if (blockIdx.x == 0) cnt[2] = cnt[4] = 0;
+      if (blockIdx.x == 0) {
+        cnt[2] = cnt[4] = 0;
+        if (s.dist_tot) s.dist_tot[3] += 1ull;
+      }
     } else {
       __threadfence();
       if (atomicAdd(cnt + 1, 1u) == gridDim.x - 1) {
-        atomicExch(cnt + 2, atomicExch(cnt, 0u));
-        atomicExch(cnt + 4, atomicExch(cnt + 3, 0u));
+        const uint32_t nl = atomicExch(cnt, 0u), nh = atomicExch(cnt + 3, 0u);
+        atomicExch(cnt + 2, nl);
+        atomicExch(cnt + 4, nh);
         atomicExch(cnt + 1, 0u);
+        if (s.dist_tot) {  // MC_FIELD_DIST_TOTALS: the cache hits were served
+          s.dist_tot[0] += nl;
+          s.dist_tot[1] += nh;
+          s.dist_tot[2] += nl - nh;
+          s.dist_tot[3] += 1ull;
+        }
       }
     }
   }

@@ -1890,6 +1890,11 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     // others, and a reset env's, go to the full transform's list)
     if (s.dist) {
       const uint64_t skip = do_reset ? ~0ull : L.sc->dist_hit;  // (and every agent with M < 0)
+      // dist_window overwrites dist_pre with the POST terms; without the
+      // prefetch every lane of the slot read all agents' PRE terms in the
+      // reward above, and in a multi-wave slot another wave may still be
+      // there: every wave passes the reward before any POST store
+      if constexpr (NT > 64 && !kPrePrefetch) __syncthreads();
       dist_window<NT, EPW, WT>(s, C, skip);
       __syncthreads();
       dlist = C.sub < N && ((((skip | L.sc->dist_fail) >> C.sub) & 1ull) || L.dm[C.sub] < 0);

@@ -122,6 +122,9 @@ struct State {
   // mc_dist.hip dist_kernel_t)
   float* dist_obs_out;
   uint32_t* dist_cnt;
+  // dist_reward: cumulative POST counters since mc_create (MC_FIELD_DIST_TOTALS):
+  // maps listed, served by the top-cell cache, fully transformed, POST launches
+  unsigned long long* dist_tot;
   // the split transform's full list (mc_dist.hip modes 1 / 2; null without
   // it): the env kernel empties it for the step (its count read by the last
   // step's mode 2 is done by then)

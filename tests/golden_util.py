@@ -15,7 +15,7 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def case_names():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith("beam_tables"))
+                  if not os.path.basename(p).startswith(("beam_tables", "known_answer")))
 
 
 def load_case(name):
@@ -108,3 +108,62 @@ def check_against_golden(env):
 
 
 
+
+
+# ---------------------------------------------------------------------------
+# The reference's published known answer (SURVEY 8(c) pin 3): BSA / BA* test
+# episodes on the hand-made grids, captured by tests/golden/make_known_answer.py
+# ---------------------------------------------------------------------------
+KNOWN_ANSWER_POLICIES = ("bsa", "ba_star")
+
+
+def load_known_answer():
+    z = np.load(os.path.join(GOLDEN_DIR, "known_answer.npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def replay_known_answer(env_cls, ka, policy):
+    """Replay every recorded test episode of ``policy`` through ``env_cls``
+    (the oracle or the HIP facade) the way ``test_RLalg`` runs it
+    (Utils/utils.py:6-44,111-149): one env over the hand-made test grids,
+    ``np.random.seed(seed)`` then ``reset(True, ind)``, then the controller's
+    recorded actions.  Observation, reward and done must equal the record at
+    every step; each episode must end done with percent_covered() == 1.0 and
+    total reward 234.  Returns the per-episode (total reward, percent covered)."""
+    pre = policy + "__"
+    config = json.loads(ka[pre + "env_config"].tobytes().decode())
+    test = [g.astype(np.float64) for g in ka["test_grids"]]
+    train = [g.astype(np.float64) for g in ka["train_grids"]]
+    with contextlib.redirect_stdout(io.StringIO()):
+        env = env_cls(train, config, use_graph=False, test_set=test)
+    n_ep = len(ka[pre + "ep_len"])
+    off = np.concatenate([[0], np.cumsum(ka[pre + "ep_len"])])
+    results = []
+    for e in range(n_ep):
+        ind, seed = int(ka[pre + "ep_grid"][e]), int(ka[pre + "ep_seed"][e])
+        tag = f"{policy} episode {e} (test grid {ind}, seed {seed})"
+        np.random.seed(seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obs, grid = env.reset(True, ind)
+        np.testing.assert_array_equal(grid, np.pad(test[ind], 1, constant_values=-1), err_msg=tag)
+        assert (int(env._xinds[0]), int(env._yinds[0])) == tuple(ka[pre + "ep_start"][e]), tag
+        np.testing.assert_array_equal(np.asarray(obs[0], np.float64), ka[pre + "obs0"][e], err_msg=tag + " reset obs")
+        total, done, steps = 0.0, False, 0
+        for t in range(off[e], off[e + 1]):
+            assert not done, (tag, "record continues after done")
+            with contextlib.redirect_stdout(io.StringIO()):
+                obs, r, done = env.step(int(ka[pre + "actions"][t]))
+            steps += 1
+            stag = f"{tag} step {steps}"
+            np.testing.assert_array_equal(np.asarray(obs[0], np.float64), ka[pre + "obs"][t], err_msg=stag + " obs")
+            assert float(r) == float(ka[pre + "rewards"][t]), (stag, float(r), float(ka[pre + "rewards"][t]))
+            assert bool(done) == bool(ka[pre + "dones"][t]), stag
+            if env._currstep == env._test_maxsteps:  # utils.py:20-21
+                done = True
+            total += r
+        pc = env.percent_covered()
+        assert done, tag
+        assert total == ka[pre + "ep_total"][e] == 234.0, (tag, total)
+        assert pc == ka[pre + "ep_pc"][e] == 1.0, (tag, pc)
+        results.append((total, pc))
+    return results

@@ -142,3 +142,43 @@ def test_rollout_matches_steps_and_oracle(torch_cuda):
     assert int(done_r.sum()) >= B  # maxsteps 9 over 24 steps
     for e in envs:
         e.check()
+
+
+def test_rollout_per_step_adjacency_and_float_layers(torch_cuda):
+    """rollout on a comm-graph config returns every step's adjacency
+    (dec_grid_rl.py:374-391 after each step's moves), equal to K step calls;
+    a dist_reward config (one registered float obs buffer) is refused rather
+    than silently keeping only the last step's float layer; mc_step_many
+    rejects a reward stride that is not a multiple of 8."""
+    import marlcov
+    torch = torch_cuda
+    c = cfg(numrobot=4, maxsteps=7, comm_radius=5, allow_comm=1)
+    rs = np.random.RandomState(5)
+    B, K = 6, 15
+    grids = [np.where(rs.rand(18, 18) < 0.1, -1.0, 1.0) for _ in range(B)]
+    envs = [marlcov.BatchCoverageEnv(c, B, grids=grids, auto_reset=True, seed=4, want_adjacency=True)
+            for _ in range(2)]
+    for e in envs:
+        e.reset()
+    acts = torch.from_numpy(rs.randint(0, 4, size=(K, B, 4)).astype(np.uint8)).to(envs[0].device)
+    (obs_r, adj_r), rew_r, done_r = envs[0].rollout(acts)
+    assert tuple(adj_r.shape) == (K, B, 4, 4)
+    changed = 0
+    for k in range(K):
+        (o, a), r, d = envs[1].step(acts[k])
+        assert torch.equal(o, obs_r[k]) and torch.equal(a, adj_r[k]), k
+        assert torch.equal(r, rew_r[k]) and torch.equal(d, done_r[k]), k
+        changed += int(k > 0 and not torch.equal(adj_r[k], adj_r[k - 1]))
+    assert changed > 0  # the graph moves with the robots: per-step values, not the last one repeated
+    assert torch.equal(envs[0].adj, adj_r[-1])
+    dc = cfg(numrobot=2, dist_reward=1, sensor_config={"num_lasers": 9, "range": 4})
+    de = marlcov.BatchCoverageEnv(dc, 2, grids=grids[:2], auto_reset=True)
+    de.reset()
+    with pytest.raises(ValueError, match="float obs"):
+        de.rollout(torch.zeros((3, 2, 2), dtype=torch.uint8, device=de.device))
+    e = envs[1]
+    rc = e.lib.mc_step_many(e._h, acts.data_ptr(), B * 4, 1, e.reward.data_ptr(), 4, e.done.data_ptr(), 0,
+                            e.obs.data_ptr(), 0, None, 0, e._stream())
+    assert rc != 0 and b"multiple of 8" in e.lib.mc_last_error()
+    for x in envs + [de]:
+        x.check()

@@ -9,7 +9,8 @@ import zlib
 import numpy as np
 import pytest
 
-from golden_util import case_names, check_against_golden, load_case, make_env, replay
+from golden_util import (KNOWN_ANSWER_POLICIES, case_names, check_against_golden, load_case, load_known_answer,
+                         make_env, replay, replay_known_answer)
 from gpu_util import compare_env, device_state, oracle_from_device, ref_action
 from oracle.cpu_ref import DecGridRLRef
 
@@ -45,6 +46,24 @@ def test_facade_matches_reference_golden(torch_cuda, name):
     case = load_case(name)
     env = make_env(marlcov.DecGridRL, case)
     replay(env, case, check_against_golden(env))
+
+
+@pytest.mark.parametrize("policy", KNOWN_ANSWER_POLICIES)
+def test_facade_known_answer(torch_cuda, policy):
+    """SURVEY 8(c) pin 3, the reference's only published result: the BSA and
+    BA* controllers (Policies/bsa.py:14, Policies/ba_star.py:10) cover 100 %
+    of the hand-made test grids (Utils/gridmaker.py:23-43) with total reward
+    234 (Example_Experiments/Non_Learning/{BSA,BA_Star}/Example/
+    TerminalOutput.txt).  Their recorded test episodes (captured from the
+    reference under the example configs: square sensor r=1,
+    single_square_tool, dijkstra_input, egoradius 1) replay through the HIP
+    facade with the observation, reward and done of every step equal to the
+    record -- so the controllers, deterministic functions of those
+    observations, drop in unchanged and reach the same answer."""
+    import marlcov
+    ka = load_known_answer()
+    res = replay_known_answer(marlcov.DecGridRL, ka, policy)
+    assert len(res) == 12 and all(r == (234.0, 1.0) for r in res)
 
 
 # ---------------------------------------------------------------------------
@@ -522,6 +541,24 @@ def test_batch_matches_oracle_ray_march(torch_cuda, name, monkeypatch):
     """The dense cases with the ray march (MARLCOV_FAN=0) instead of the
     sector march."""
     monkeypatch.setenv("MARLCOV_FAN", "0")
+    test_batch_matches_oracle(torch_cuda, name)
+
+
+@pytest.mark.parametrize("name", ["dist_lidar_n3", "dist_long_walk", "dist_single_tool", "dist_map_sharing"])
+def test_batch_dist_multi_wave_slot(torch_cuda, name, monkeypatch):
+    """dist_reward configs forced onto a 4-wave workgroup (MARLCOV_NT=256) on
+    the generic kernel, where every lane reads all agents' PRE terms in the
+    reward and dist_window then overwrites them with the POST terms
+    (dec_grid_rl.py:222-223,239-240): the waves of a slot must all pass the
+    reward before any POST store."""
+    monkeypatch.setenv("MARLCOV_NT", "256")
+    import marlcov
+    cfg, maker, B, _ = BATCH_CASES[name]
+    rs = np.random.RandomState(1)
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=[maker(rs) for _ in range(B)], auto_reset=False)
+    v = env.kernel_variant()
+    assert v.startswith("env_kernel<256,1,") and "generic>" in v, v
+    del env
     test_batch_matches_oracle(torch_cuda, name)
 
 

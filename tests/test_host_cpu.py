@@ -144,6 +144,23 @@ def test_bench_bytes_formula_matches_survey():
     assert bench.algorithmic_bytes_per_env_step(1, 10, 2) == 893
     assert bench.algorithmic_bytes_per_env_step(4, 10, 2) == 3476
     assert bench.algorithmic_bytes_per_env_step(8, 20, 2) == 24280
+    # C5: SURVEY 8(d)'s figure (a full-map read per agent and step) ...
+    assert bench.algorithmic_bytes_per_env_step(16, 10, 2, layers=7, full_map_cells=518 ** 2) == 1088720
+
+
+def test_c5_design_bytes_formula():
+    """The C5 bench line's roofline bytes: the windowed 8(d)
+    part, 16 x (441 + 336 + 175 + 9) + 32 = 15,408 B per env-step, plus per
+    step the maps fully transformed (ceil(518^2 / 8) = 33,541 B bit-map read
+    + 4,128 B cache write), the maps the cache served (4,128 B cache read) and
+    4 B per listed map, from the MC_FIELD_DIST_TOTALS deltas."""
+    import bench
+    f = bench.c5_design_bytes_per_step
+    assert f(1, 16, 10, 2, 518, 0, 0, 0, 1) == 15408
+    assert bench.DIST_CACHE_BYTES == 4128
+    # 100 listed over 2 launches: 60 served, 40 full transforms
+    extra = 40 * (33541 + 4128) + 60 * 4128 + 100 * 4
+    assert f(8192, 16, 10, 2, 518, 100, 60, 40, 2) == 8192 * 15408 + extra / 2
 
 
 def test_tile_block_layout_round_trip():

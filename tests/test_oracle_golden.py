@@ -3,7 +3,8 @@ the real reference (tests/golden/make_golden.py).  Bit-exact on every field."""
 import numpy as np
 import pytest
 
-from golden_util import GOLDEN_DIR, case_names, check_against_golden, load_case, make_env, replay
+from golden_util import (GOLDEN_DIR, KNOWN_ANSWER_POLICIES, case_names, check_against_golden, load_case,
+                         load_known_answer, make_env, replay, replay_known_answer)
 from oracle.cpu_ref import DecGridRLRef, lidar_beam_table, lidar_thetas
 from oracle.super_ref import SuperGridRLRef
 from super_golden_util import (check_super_golden, load_super_case, make_super_env, replay_super,
@@ -49,3 +50,15 @@ def test_golden_inventory():
     for must in ("c1_empty32", "lidar_n4_48", "lidar_360_r20", "joint_n16",
                  "sentinels_and_odd_actions", "map_sharing_n4", "comm_graph_n4"):
         assert must in names
+
+
+@pytest.mark.parametrize("policy", KNOWN_ANSWER_POLICIES)
+def test_oracle_known_answer(policy):
+    """SURVEY 8(c) pin 3, the reference's published result: BSA / BA* cover
+    100 % of every hand-made test grid with total reward 234
+    (Example_Experiments/Non_Learning/{BSA,BA_Star}/Example/TerminalOutput.txt).
+    The recorded controller trajectories replay bit-exactly on the oracle."""
+    ka = load_known_answer()
+    res = replay_known_answer(DecGridRLRef, ka, policy)
+    assert len(res) == 12 and all(r == (234.0, 1.0) for r in res)
+    assert sorted(set(ka[policy + "__ep_grid"].tolist())) == [0, 1, 2]
