@@ -262,6 +262,9 @@ def main():
                          "launch per step); stream: K back-to-back Python/ctypes mc_step calls; graph: "
                          "uploaded hipGraph replay; events: per-launch HIP events")
     ap.add_argument("--eager", action="store_true", help="alias of --launch events")
+    ap.add_argument("--sync", default="default", choices=["default", "spin"],
+                    help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is initialised, so "
+                         "the host synchronize that closes the timed region spin-waits instead of sleeping")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL over xGMI).  gloo rehearses the "
                          "multi-rank flow on fewer GPUs than ranks (ranks share the visible GPUs "
@@ -292,6 +295,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.config, args.cpu_procs, args.cpu_secs)
+
+    if args.sync == "spin":
+        set_spin_sync(local)
 
     import torch
     import torch.distributed as dist
@@ -412,6 +418,7 @@ def main():
                 "global env id)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": total_envs,
                    "launch": LAUNCH_DESC[args.launch], "host_issue_us_per_step": issue_us,
+                   "host_sync": args.sync,
                    "kernel_variant": env.kernel_variant(),
                    **dist_desc(args, world),
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
@@ -435,6 +442,19 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def set_spin_sync(local):
+    """hipDeviceScheduleSpin on this rank's device, before torch creates its
+    context (a no-op flag for the work itself: the host's wait for the last
+    kernel spins instead of yielding)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int(0)
+    assert hip.hipGetDeviceCount(ctypes.byref(n)) == 0
+    assert hip.hipSetDevice(ctypes.c_int(local % max(1, n.value))) == 0
+    rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+    assert rc == 0, f"hipSetDeviceFlags: {rc}"
 
 
 def dist_desc(args, world):
