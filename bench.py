@@ -354,7 +354,7 @@ def main():
     a0 = aptrs[0] if K else 0
     elapsed, kern_ms, issue_us = timed_launches(
         lambda i, st: env.step_raw(aptrs[i], rp, dp, op, st), dev, K, args.launch,
-        many_fn=lambda n, st: env.step_many_raw(a0, astride, n, rp, dp, op, st))
+        many_call=lambda st: native_call(env, a0, astride, K, rp, dp, op, st))
     env.check()
     listed = dj_listed = served = dtot = None
     if dr:  # maps the last step sent to the full distance transform, and those the cache served (diagnostic)
@@ -472,14 +472,29 @@ def dist_desc(args, world):
     return d
 
 
-def timed_launches(step_fn, dev, K, launch, many_fn=None):
+def native_call(env, a0, astride, K, rp, dp, op, stream_ptr):
+    """mc_step_many's K launches as a zero-argument call with every ctypes
+    argument converted beforehand (no Python marshalling between the first
+    event record and the first launch)."""
+    import ctypes
+    f = env.lib.mc_step_many
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    args = (env._h if isinstance(env._h, vp) else vp(env._h), vp(a0), i64(astride), ctypes.c_int32(K), vp(rp), i64(0),
+            vp(dp), i64(0), vp(op), i64(0), None, i64(0), vp(stream_ptr))
+    return lambda: f(*args)
+
+
+def timed_launches(step_fn, dev, K, launch, many_call=None):
     """Time K launches between barrier + synchronize; returns (elapsed s, ms
     per launch from HIP events on the launch stream, host issue time per
     step in us: from the first event record to the last launch returned).
 
-    launch = "native": one C-ABI call issues the K launches (many_fn(K,
-    stream): mc_step_many, one env-kernel launch per step, no Python or
-    ctypes per step).  "stream": the K launches are issued back to back on the stream
+    launch = "native": one C-ABI call issues the K launches (many_call(stream)
+    returns the prepared mc_step_many call: one env-kernel launch per step,
+    no Python or ctypes per step); its timing events are raw HIP events
+    recorded through ctypes (torch's Event.record adds ~8 us of Python and a
+    device guard between the first record and the first launch,
+    profiles/r5/short_form/).  "stream": the K launches are issued back to back on the stream
     (asynchronous; the host stays ahead of a ~10 us kernel, so the GPU runs
     them back to back and the first kernel starts at once).  "graph": they
     are captured into hipGraphs (chunks of 100) that are instantiated and
@@ -493,6 +508,8 @@ def timed_launches(step_fn, dev, K, launch, many_fn=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     stream = torch.cuda.current_stream(dev)
+    if launch == "native":
+        return timed_native(many_call(stream.cuda_stream), dev, K, stream, world)
     graphs = []
     if launch == "graph":
         hip = ctypes.CDLL("libamdhip64.so")
@@ -533,9 +550,6 @@ def timed_launches(step_fn, dev, K, launch, many_fn=None):
             starts[i].record(stream)
             step_fn(i, stream.cuda_stream)
             ends[i].record(stream)
-    elif launch == "native":
-        rc = many_fn(K, stream.cuda_stream)
-        assert rc == 0, rc
     else:
         for i in range(K):
             step_fn(i, stream.cuda_stream)
@@ -549,6 +563,43 @@ def timed_launches(step_fn, dev, K, launch, many_fn=None):
     if launch == "events":
         return t1 - t0, sum(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)) / K, issue_us
     return t1 - t0, ev0.elapsed_time(ev1) / K, issue_us
+
+
+def timed_native(call, dev, K, stream, world):
+    """The native timed region: raw HIP events (ctypes) around one
+    mc_step_many call, between barrier + synchronize on both sides."""
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    ev = [ctypes.c_void_p() for _ in range(2)]
+    for e in ev:
+        assert hip.hipEventCreate(ctypes.byref(e)) == 0
+    rec = hip.hipEventRecord
+    rec.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    for e in ev:  # first records outside the timed region
+        assert rec(e, sp) == 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    rec(ev[0], sp)
+    rc = call()
+    t_issue = time.perf_counter()
+    rec(ev[1], sp)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    assert rc == 0, rc
+    if world > 1:
+        dist.barrier()
+    ms = ctypes.c_float(0.0)
+    assert hip.hipEventElapsedTime(ctypes.byref(ms), ev[0], ev[1]) == 0
+    for e in ev:
+        hip.hipEventDestroy(e)
+    return t1 - t0, ms.value / K, round((t_issue - t0) / K * 1e6, 3)
 
 
 KERNEL_US_FROM = {

@@ -581,6 +581,77 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
   if (C.sub == 0) { L.sc->pen = pen; L.sc->moved = moved; }
 }
 
+#ifndef MC_MOVES_SERIAL  // A/B knob: 1 keeps the serial broadcast rounds (moves) at C5
+#define MC_MOVES_SERIAL 0
+#endif
+
+// Same moves for a compile-time agent count NS > 8 with one env per
+// workgroup (C5: 16 robots), by a fixed point instead of N serial broadcast
+// rounds.  Robot i moves iff its action is a move (0..3), its target is not
+// blocked (grid < 0, out of bounds) and no robot sits on the target at its
+// turn: robots j < i at their final cells, robots j > i at their starting
+// cells (:186,190-199,310).  So robot i's outcome depends only on the
+// outcomes of robots j < i: iterating "moves = ok0 and target not occupied
+// under the previous iterate's cells" fixes robot 0 after one round, robot 1
+// after two, ..., and the true outcome is the iteration's only fixed point.
+// Starting from "every unblocked robot moves", a step without a conflict
+// between robots ends after one round and its check.  Lane i = robot i of
+// the first wave; each round is NS compares per lane against the robots'
+// cells read as scalars (v_readlane), one ballot.
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void moves_par(const State& s, const Ctx<NT, EPW, WT>& C, double pen_unit) {
+  static_assert(EPW == 1 && NS > 0 && NS <= 64, "one env per workgroup, compile-time robots <= 64");
+  const Lds<WT>& L = C.L;
+  const int i = C.sub;  // lane of the first wave
+  const bool live = i < NS;
+  const int x = live ? L.x0[i] : 0, y = live ? L.y0[i] : 0;
+  const int act = live ? (int)L.act[i] : 255;
+  const int dx = (act == 0) - (act == 2), dy = (act == 1) - (act == 3);
+  bool blk = true;
+  if (live && act < 4) {
+    const int lx = x + dx - 8 * L.bx[i], ly = y + dy - 8 * L.by[i];
+    blk = ((L.negr[row_word<WT>(s, i, lx)] >> ly) & (WT)1) != 0;
+  }
+  const bool acts = live && act <= 3;  // not 0..3: no updateRobotPos call, no penalty
+  const bool ok0 = acts && !blk;
+  // cells packed x | y << 16 (padded-grid coordinates, < 2^16; a target is
+  // inside the -1 border, so no coordinate is negative)
+  const uint32_t X = (uint32_t)x | ((uint32_t)y << 16);
+  const uint32_t T = (uint32_t)(x + dx) | ((uint32_t)(y + dy) << 16);
+  uint32_t XA[NS], TA[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    XA[j] = (uint32_t)rdlane((int)X, j);
+    TA[j] = (uint32_t)rdlane((int)T, j);
+  }
+  uint64_t cm = __ballot(ok0);  // bit j: robot j moves (the iterate)
+  bool c = ok0;
+  for (int it = 0; it <= NS; ++it) {  // (at most NS + 1 rounds; ~2 in practice)
+    bool occ = false;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const uint32_t pj = ((cm >> j) & 1ull) ? TA[j] : XA[j];  // robot j's final cell under the iterate
+      occ |= (j < i ? pj : XA[j]) == T;                         // (j == i: X != T for a move)
+    }
+    c = ok0 && !occ;
+    const uint64_t nm = __ballot(c);
+    if (nm == cm) break;
+    cm = nm;
+  }
+  if (live) {
+    L.x[i] = c ? x + dx : x;
+    L.y[i] = c ? y + dy : y;
+  }
+  // reward += -collision_penalty per failed move, in robot order (:203)
+  const int fails = __popcll(__ballot(acts && !c));
+  if (i == 0) {
+    double pen = 0.0;
+    for (int k = 0; k < fails; ++k) pen += pen_unit;
+    L.sc->pen = pen;
+    L.sc->moved = L.sc->moved | cm;
+  }
+}
+
 // Same moves for a compile-time agent count NS <= 8: every lane of the slot
 // replays the robot-order loop on all robots' data in registers (no
 // cross-lane traffic); lane 0 publishes the result.
@@ -1114,6 +1185,10 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
   const int jl = jw < s.N ? jw : 0;
   const int abx = L.bx[jl], aby = L.by[jl];
   uint32_t cf = 0, cv = 0;
+#ifdef MC_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(14);  // the staged mask tiles landed
+#endif
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
     const int idx = C.sub + k * LPE;
@@ -1803,6 +1878,8 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       // per env kernel, profiles/r4/c5_grid/)
       if constexpr (SH::N > 0 && SH::N <= 8) {
         if (NT == 64 || C.sub < 64) moves_regs<NT, EPW, WT, SH::N>(s, C, -s.pen);
+      } else if constexpr (SH::N > 8 && EPW == 1 && !MC_MOVES_SERIAL) {
+        if (C.sub < 64) moves_par<NT, EPW, WT, SH::N>(s, C, -s.pen);
       } else if (C.sub < 64) {
         moves<NT, EPW, WT>(s, C, -s.pen);
       }

@@ -225,6 +225,58 @@ def test_c5_shape_512_per_step(torch_cuda):
     run_against_oracle(torch, env, cfg, rs, 30, sample, 5, "c5_512", dist_check=True, sentinel_p=0.0)
 
 
+@pytest.mark.parametrize("dist", [0, 1])
+def test_c5_shape_crowded_collisions(torch_cuda, dist):
+    """The C5 instantiation's moves (16 robots: moves_par's fixed point over
+    the robot order) where robots block each other all the time: 16 robots
+    on 12 x 12 grids, every step against the oracle (dec_grid_rl.py:171-204,
+    284-310: a robot may enter a cell a lower-index robot vacated this step
+    and is blocked by a higher-index robot that has not moved yet).  The
+    oracle counts the robot-robot blocks; there must be many, including
+    chains (a block that depends on another robot's outcome this step)."""
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, maxsteps=25, dist_reward=dist, collision_penalty=2.5)
+    rs = np.random.RandomState(1616 + dist)
+    B, N, T = 16, 16, 40
+    grids = [bern(rs, 12, 12, 0.15) for _ in range(B)]
+    env = marlcov.BatchCoverageEnv(cfg, B, grids=grids, auto_reset=True, seed=16)
+    assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    st = device_state(env)
+    refs = {b: oracle_from_device(st, b, cfg) for b in range(B)}
+    blocks = chains = 0
+    for t in range(T):
+        acts = rs.randint(0, 4, size=(B, N)).astype(np.uint8)
+        acts[rs.rand(B, N) < 0.05] = 7
+        obs, rew, done = env.step(torch.from_numpy(acts).to(env.device))
+        obs_h, rew_h, done_h = full_obs(env, obs, cfg), rew.cpu().numpy(), done.cpu().numpy()
+        st = device_state(env)
+        for b in range(B):
+            ref = refs[b]
+            x0, y0 = ref._xinds.copy(), ref._yinds.copy()
+            start = {(int(x0[i]), int(y0[i])): i for i in range(N)}
+            o, r, d = ref.step(ref_action(acts[b]))
+            for i in range(N):
+                a = int(acts[b, i])
+                if a > 3 or (ref._xinds[i], ref._yinds[i]) != (x0[i], y0[i]):
+                    continue
+                tx, ty = x0[i] + (a == 0) - (a == 2), y0[i] + (a == 1) - (a == 3)
+                if ref._grid[tx, ty] >= 0:  # free target: another robot blocked it
+                    blocks += 1
+                    j = start.get((int(tx), int(ty)))
+                    chains += int(j is not None and j < i)  # j < i stayed: its own outcome decided i's
+            tag = f"c5 crowded t={t} env {b}"
+            assert float(r) == rew_h[b], (tag, float(r), rew_h[b])
+            assert bool(d) == bool(done_h[b]), tag
+            if d:
+                o, _ = ref.reset(False, None, positions=[tuple(q) for q in st["pos"][b]])
+            np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
+            compare_env(st, b, ref, tag)
+    assert blocks > 200 and chains > 20, (blocks, chains)
+    env.check()
+
+
 def test_c5_top_cell_cache_is_exact(torch_cuda, monkeypatch):
     """The dist_reward top-cell cache (mc_dist.hip: the cells with d >= M -
     kDistT, T = 20, and the box of cells covered since) against the full

@@ -30,12 +30,13 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--lib", default=LIB, help="a stamped library (tools/build_variants.py NAME:-DMC_STAMPS ...)")
     args = ap.parse_args()
-    if args.build_only or not os.path.exists(LIB):
+    if args.lib == LIB and (args.build_only or not os.path.exists(LIB)):
         build()
         if args.build_only:
             return
-    os.environ["MARLCOV_LIB"] = LIB
+    os.environ["MARLCOV_LIB"] = args.lib
     print("library:", os.environ["MARLCOV_LIB"])
     import numpy as np
     import torch
@@ -79,7 +80,8 @@ def main():
         d = s[ok, j] - s[ok, i]
         print(f"  {name:22s} median {np.median(d):8.0f}  p90 {np.percentile(d,90):8.0f}  max {d.max():8d}  n={ok.sum()}")
     for (i, j), name in [((1, 11), "stage: issue"), ((11, 12), "stage: wait"), ((12, 2), "stage: lds"),
-                         ((3, 13), "sense: march"), ((13, 4), "sense: gather")]:
+                         ((3, 13), "sense: march"), ((13, 4), "sense: gather"),
+                         ((4, 14), "merge: mask wait"), ((14, 5), "merge: work+barrier")]:
         ok = (s[:, i] > 0) & (s[:, j] > 0)
         if ok.any():
             d = s[ok, j] - s[ok, i]
