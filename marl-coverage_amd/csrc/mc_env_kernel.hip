@@ -1184,6 +1184,30 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
   const int jw = (int)(threadIdx.x & 63);
   const int jl = jw < s.N ? jw : 0;
   const int abx = L.bx[jl], aby = L.by[jl];
+  // EPW == 1 without a compile-time agent count <= 8 (C5: 16 agents):
+  // lane j (< N) of every wave holds ovj, bit b = a lower-index agent b whose
+  // block overlaps agent j's; an item fetches its agent's mask from lane a
+  // (ds_bpermute) and reads only those agents' marks -- usually none, where
+  // the loop over every lower agent ran up to N - 1 readlane rounds per item
+  uint64_t ovj = 0;
+  if constexpr (NS == 0 && EPW == 1) {
+    for (int b = 0; b < s.N - 1; ++b) {  // uniform trip count (unrolled when N is compiled in)
+      const int bxb = rdlane(abx, b), byb = rdlane(aby, b);
+      const bool ov = b < jw && abs(abx - bxb) < TW && abs(aby - byb) < TW;
+      ovj |= ov ? (1ull << b) : 0ull;
+    }
+  }
+  // (fetched with every lane active: ds_bpermute reads 0 from inactive lanes)
+  uint64_t ova[KI];
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    ova[k] = 0;
+    if constexpr (NS == 0 && EPW == 1) {
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)ovj, I.a[k]);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(ovj >> 32), I.a[k]);
+      ova[k] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+  }
   uint32_t cf = 0, cv = 0;
 #ifdef MC_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1231,18 +1255,17 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
         }
 #pragma unroll
         for (int b = 0; b < NS - 1; ++b) cand &= ~t[b];
+      } else if constexpr (EPW == 1) {
+        for (uint64_t m = ova[k]; m; m &= m - 1ull) {
+          const int b = __ffsll((unsigned long long)m) - 1;
+          const int bi = gi - L.bx[b], bj = gj - L.by[b];
+          if ((unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW)
+            cand &= ~L.fp[(b * TW + bi) * TW + bj];
+        }
       } else {
       for (int b = 0; b < s.N - 1; ++b) {
         if (b >= a) break;
-        int bxb, byb;
-        if constexpr (EPW == 1) {
-          bxb = rdlane(abx, b);
-          byb = rdlane(aby, b);
-        } else {
-          bxb = L.bx[b];
-          byb = L.by[b];
-        }
-        const int bi = gi - bxb, bj = gj - byb;
+        const int bi = gi - L.bx[b], bj = gj - L.by[b];
         if ((unsigned)bi < (unsigned)TW && (unsigned)bj < (unsigned)TW)
           cand &= ~L.fp[(b * TW + bi) * TW + bj];
       }
@@ -1604,7 +1627,8 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
   using OF = ObsFast<EGO, NS, LC>;
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   constexpr int E = OF::E, EE = OF::EE, NB = OF::NB;
-  static_assert(NB <= LPE, "one crop per lane");
+  static_assert(NB <= LPE && NB <= 64, "one crop per lane of the first wave");
+  static_assert(NT == 64 || EPW == 1, "one wave, or one env per workgroup");
   const Lds<WT>& L = C.L;
   const int TW = s.TW;
   // ---- crops
@@ -1633,7 +1657,38 @@ __device__ __forceinline__ void write_obs_fast(const State& s, const Ctx<NT, EPW
     const uint32_t w = (uint32_t)p[0] | ((uint32_t)p[8] << 8);
     fo |= ((w >> (ly0 & 7)) & ((1u << E) - 1u)) << (r * E);
   }
-  const uint32_t crop = layer == 0 ? rp : (layer <= 2 ? fo : 0u);  // layer 3: dijkstra
+  const uint32_t crop = layer == 0 ? rp : (layer <= 2 ? fo : 0u);  // layer 3: dijkstra / dist (float buffer)
+  if constexpr (NT > 64) {
+    // one env per multi-wave workgroup (C4, C5): the first wave's crops go
+    // through LDS (the march's dead sink row) to every lane; lane l writes
+    // bits [16 l, 16 l + 16) of the env's crop stream as one dwordx4 (16
+    // bits span at most two crops: EE >= 16), else dword by dword
+    uint32_t* cl = reinterpret_cast<uint32_t*>(L.sink);
+    if (C.sub < NB) cl[C.sub] = crop;
+    __syncthreads();
+    constexpr int DPE = NB * EE / 4;
+    uint32_t* out = reinterpret_cast<uint32_t*>(obs_out + (size_t)C.e * (NB * EE));
+    if constexpr (DPE % 4 == 0 && EE >= 16) {
+      for (int q = C.sub; q < DPE / 4; q += NT) {
+        const int i = 16 * q, jb = i / EE, o = i - jb * EE;
+        const uint64_t w = (uint64_t)cl[jb] | ((uint64_t)(jb + 1 < NB ? cl[jb + 1] : 0u) << EE);
+        const uint32_t bits = (uint32_t)(w >> o);
+        uint4 v;
+        v.x = ((bits & 0xFu) * 0x00204081u) & 0x01010101u;
+        v.y = (((bits >> 4) & 0xFu) * 0x00204081u) & 0x01010101u;
+        v.z = (((bits >> 8) & 0xFu) * 0x00204081u) & 0x01010101u;
+        v.w = (((bits >> 12) & 0xFu) * 0x00204081u) & 0x01010101u;
+        reinterpret_cast<uint4*>(out)[q] = v;
+      }
+    } else {
+      for (int d = C.sub; d < DPE; d += NT) {
+        const int i = 4 * d, jb = i / EE, o = i - jb * EE;
+        const uint64_t w = (uint64_t)cl[jb] | ((uint64_t)(jb + 1 < NB ? cl[jb + 1] : 0u) << EE);
+        out[d] = ((uint32_t)(w >> o) & 0xFu) * 0x00204081u & 0x01010101u;
+      }
+    }
+    return;
+  }
   // ---- dwords of the wave's obs run
   constexpr int DPE = NB * EE / 4;       // dwords per env (a cell is one byte)
   constexpr int D = EPW * DPE;           // dwords per wave
@@ -1767,11 +1822,23 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   const int4 fv0 = fsrc[C.sub < n16 ? C.sub : 0];
   const int4 fv1 = fsrc[C.sub + LPE < n16 ? C.sub + LPE : 0];
   const int4 fv2 = fsrc[C.sub + 2 * LPE < n16 ? C.sub + 2 * LPE : 0];
+  // dist_reward: M and witness of each free map, and the top-cell cache's
+  // count and box (mc_internal.h State::dist_ch), in the same round trip
+  const int agd = C.sub < N ? C.sub : 0;
+  int2 mwv = make_int2(-1, 0);
+  int4 chd = make_int4(-1, 0, 0, 0);
+  int2 chb = make_int2(0, 0);
+  if (s.dist) mwv = reinterpret_cast<const int2*>(s.dist_mw)[eN + agd];
+  if (s.dist_ch) {
+    const int4* hp = reinterpret_cast<const int4*>(s.dist_ch + ((size_t)eN + agd) * 8);
+    chd = hp[0];
+    chb = *reinterpret_cast<const int2*>(hp + 1);
+  }
   zero_marks<NT, EPW, WT>(s, C);  // overlaps the round trip
   // every result is needed below: keep the compiler from sinking a load into
   // the branch that uses it (that would make it a round trip of its own)
   asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(act_raw), "v"(act0_raw), "v"(req_raw), "v"(g0),
-               "v"(bm0.x), "v"(bm0.w));
+               "v"(bm0.x), "v"(bm0.w), "v"(mwv.x), "v"(mwv.y), "v"(chd.x), "v"(chd.w), "v"(chb.y));
   const int act = is_step ? act_raw : 255;
   const int act0 = is_step ? act0_raw : 0;      // agent 0's byte: the sentinel
   const int req = env_mask != nullptr ? req_raw : 1;
@@ -1798,19 +1865,11 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     L.sc->zero = 0;
   }
   if (s.dist && C.sub < N) {  // dist_reward: M and witness of each free map
-    const int2 mw = reinterpret_cast<const int2*>(s.dist_mw)[(size_t)e * N + C.sub];
-    L.dm[C.sub] = mw.x;
-    L.dw[C.sub] = mw.y;
+    L.dm[C.sub] = mwv.x;
+    L.dw[C.sub] = mwv.y;
   }
-  // dist_reward top-cell cache: count and box of agent C.sub's cache (the
-  // box grows by this step's sensing window, mc_internal.h State::dist_ch)
-  int4 chd = make_int4(-1, 0, 0, 0);
-  int2 chb = make_int2(0, 0);
-  if (s.dist_ch && C.sub < N) {
-    const int4* hp = reinterpret_cast<const int4*>(s.dist_ch + ((size_t)e * N + C.sub) * 8);
-    chd = hp[0];
-    chb = *reinterpret_cast<const int2*>(hp + 1);
-  }
+  // (chd / chb: the top-cell cache of agent C.sub; its box grows by this
+  // step's sensing window below)
   if (fan) {
     int4* dst = reinterpret_cast<int4*>(L.fan);
     if (C.sub < n16) dst[C.sub] = fv0;
@@ -2055,9 +2114,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     }
   }
   STAMP(8);
-  if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && NT == 64 &&
-                ObsFast<SH::EGO, SH::N, SH::LC>::NB <= CtxT::LPE) {
-    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the wave
+  if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && (NT == 64 || EPW == 1) &&
+                ObsFast<SH::EGO, SH::N, SH::LC>::NB <= 64) {
+    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the workgroup
   } else {
     if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 16) ? SH::N : 0>(s, C, obs_out);
   }
@@ -2115,7 +2174,7 @@ using Dynamic = Shape<0, 0, 0, 0, 0>;
 using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;      // the bench workload
 using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs layers)
 using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;    // 360 beams, R=20
-using ShapeC5 = Shape<16, 10, 21, 0, 10, 8>;     // 16 agents, dist_reward (4 obs layers)
+using ShapeC5 = Shape<16, 10, 21, 2, 10, 8, 4, 1>;  // 16 agents, egoradius 2, dist_reward (4 obs layers)
 
 #define MC_EL(T, P, W, SH, NAME) \
   EnvLaunch { "env_kernel<" #T "," #P "," NAME ">", &launch_one<T, P, W, SH> }

@@ -255,14 +255,16 @@ __host__ __device__ inline size_t slot_stride(size_t slot_lds) {
 // unrolls); 0 leaves the field to the runtime State.  The launcher picks a
 // specialised instantiation only when the runtime State matches it exactly.
 // LC: obs layers of an EGO shape (3; 4 with dijkstra_input, whose layer 3 the
-// dijkstra kernel writes after the env kernel).
-template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3>
+// dijkstra kernel writes after the env kernel, or with dist_reward, whose
+// layer 3 is the float buffer: 0 in the uint8 obs).  DS: an EGO shape's
+// dist_reward flag (baked in).
+template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3, int DS_ = 0>
 struct Shape {
-  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_, LC = LC_;
+  static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_, LC = LC_, DS = DS_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
            (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
-           (EGO_ == 0 || (s.ego == EGO_ && s.Lc == LC_ && !s.dist)) &&
+           (EGO_ == 0 || (s.ego == EGO_ && s.Lc == LC_ && (s.dist != 0) == (DS_ != 0))) &&
            (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_)) &&
            (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_));
   }
@@ -296,7 +298,7 @@ __device__ __forceinline__ void specialize(State& s) {
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
   if constexpr (SH::KN > 0) s.beam_kmin = SH::KN;
-  if constexpr (SH::EGO > 0) s.dist = 0;  // EGO shapes match only configs without dist_reward
+  if constexpr (SH::EGO > 0) s.dist = SH::DS;  // an EGO shape bakes in its dist_reward flag
 }
 
 }  // namespace mc
