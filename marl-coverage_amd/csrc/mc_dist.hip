@@ -195,6 +195,44 @@ __device__ __forceinline__ int row_near(uint64_t row, int c) {
   return h;
 }
 
+// Hand-off between the parts of a split map inside one launch (the fused
+// mode 2, MI355X_MICROARCH.md: the fan-in row of the hand-off table): the
+// parts store the handed-off words `sc1` (agent-scope relaxed atomic stores
+// lower to global_store ... sc1: write-through past the XCD's L2), every
+// storing wave waits for its stores, and after a workgroup barrier one lane
+// adds to the map's counter (agent scope); the part whose add returns S - 1
+// loads them back `sc1` (global_load ... sc1: past its L1).  Global address
+// space casts keep them global_ (never flat_) instructions.
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((g_u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) { st_sc1(reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
+__device__ __forceinline__ void st_sc1(int2* p, int2 v) {
+  __hip_atomic_store((g_u64*)p, (unsigned long long)(uint32_t)v.x | ((unsigned long long)(uint32_t)v.y << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) { return __uint_as_float(ld_sc1(reinterpret_cast<const uint32_t*>(p))); }
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
+  return __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int2 ld_sc1(const int2* p) {
+  const unsigned long long v = ld_sc1(reinterpret_cast<const unsigned long long*>(p));
+  return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+}
+// plain or `sc1`
+template <typename T>
+__device__ __forceinline__ T ld_ho(const T* p, bool sc1) { return sc1 ? ld_sc1(p) : *p; }
+template <typename T>
+__device__ __forceinline__ void st_ho(T* p, T v, bool sc1) {
+  if (sc1) st_sc1(p, v);
+  else *p = v;
+}
+
 // max over the wave (every lane gets it)
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
@@ -486,6 +524,12 @@ constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
 #endif
 constexpr int kMaxParts = MC_MAX_PARTS;
 constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
+#ifndef MC_DIST_FUSED  // build knob (A/B): 0 finalises split maps in a separate mode-3 launch
+#define MC_DIST_FUSED 1
+#endif
+// the part of a split map that finishes last finalises it inside mode 2
+// (`sc1` hand-off of the partials) instead of a mode-3 launch after it
+constexpr bool kFused = MC_DIST_FUSED != 0;
 
 template <int kCL>
 __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
@@ -608,21 +652,26 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // before it failed): a lower bound of the new max(d)
     const int theta0 = mode >= 2 ? (int)full[9 + 2 * fi] : ((s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0);
     bool need_cb = true;  // the map's bitboard in LDS
-    if (mode == 3) {
-      // ---- merge the parts' partials: the best key, the raw target d (in
-      // the output buffers), the strip maxima, the cache candidates
-      __syncthreads();  // the item's LDS scalars are initialised
+    // ---- merge a split map's parts' partials: the best key, the raw target
+    // d (in the output buffers), the strip maxima, the cache candidates.
+    // Mode 3 (a launch after mode 2: plain loads), or the part of a fused
+    // mode 2 that finished last (`sc1` loads of the parts' `sc1` stores)
+    auto merge_parts = [&](bool sc1) {
+      __syncthreads();  // the item's LDS scalars are initialised; every thread is past its own list
+      if (tid == 0) s_ccount = 0;
+      __syncthreads();
       // the parts' candidates: a one-pass list (with theta0), else none
-      const uint32_t total = (kOnePass && theta0 > 0) ? s.dist_gcnt[ea] : 0u;
-      const unsigned long long gk = s.dist_gkey[ea];
+      const uint32_t total = (kOnePass && theta0 > 0) ? ld_ho(s.dist_gcnt + ea, sc1) : 0u;
+      const unsigned long long gk = ld_ho(s.dist_gkey + ea, sc1);
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
       for (int t = tid; t < T; t += kDtThreads)
-        s_d[t] = (int)(t < 5 ? pre_out[(size_t)ea * 8 + 1 + t] : dist_obs[(size_t)ea * E * E + (t - 5)]);
+        s_d[t] = (int)(t < 5 ? ld_ho(pre_out + (size_t)ea * 8 + 1 + t, sc1)
+                             : ld_ho(dist_obs + (size_t)ea * E * E + (t - 5), sc1));
       for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
-        s_smax[st] = s.dist_sm[(size_t)ea * kMaxTrack + st];
+        s_smax[st] = (int)ld_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, sc1);
       if (gk != 0 && total <= (uint32_t)kGCand)
         for (int k = tid; k < (int)total; k += kDtThreads) {
-          const int2 c = s.dist_gcand[(size_t)ea * kGCand + k];
+          const int2 c = ld_ho(s.dist_gcand + (size_t)ea * kGCand + k, sc1);
           if (c.y >= thr) {
             const int j = atomicAdd(&s_ccount, 1);
             if (j < kDistK) {
@@ -640,6 +689,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s.dist_gcnt[ea] = 0;
       }
       __syncthreads();
+    };
+    if (mode == 3) {
+      merge_parts(false);
       need_cb = s_cov && !(kOnePass && theta0 > 0 && s_ccount <= kDistK);  // the second pass
     }
     if (!fast && need_cb) {
@@ -913,7 +965,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // order of their bound with the exact maxima so far as the bound, a
     // barrier per strip: slower, 263 vs 242 us per step at C5.)
     const bool prune = theta0 > 0 && nstrips_all <= kMaxTrack;
-    const uint16_t* smb = s.dist_ch ? s.dist_sm + (size_t)ea * kMaxTrack : nullptr;
+    const uint32_t* smb = s.dist_ch ? s.dist_sm + (size_t)ea * kMaxTrack : nullptr;
     int runmax = 0;
     uint64_t ran = 0;  // strips transformed (their s_smax are exact maxima)
     const int s_from = nstrips > 0 ? st_lo : 0, s_to = nstrips > 0 ? st_hi : 0;
@@ -971,18 +1023,19 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                             ((unsigned long long)ubest << 16) | (unsigned long long)vbest);
     }
     __syncthreads();
+    bool merged = false;  // this part finalises its split map (fused mode 2)
     if (mode == 2 && S > 1) {
       // ---- a part: publish the best key, the targets it holds (raw d in
       // the output buffers), its strips' maxima and its cache candidates;
-      // mode 3 finalises the map
+      // the part that finishes last (fused) or mode 3 finalises the map
       if (tid == 0 && s_key) atomicMax(s.dist_gkey + ea, s_key);
       for (int t = tid; t < T; t += kDtThreads)
         if (s_d[t] >= 0) {
-          if (t < 5) pre_out[(size_t)ea * 8 + 1 + t] = (float)s_d[t];
-          else dist_obs[(size_t)ea * E * E + (t - 5)] = (float)s_d[t];
+          if (t < 5) st_ho(pre_out + (size_t)ea * 8 + 1 + t, (float)s_d[t], kFused);
+          else st_ho(dist_obs + (size_t)ea * E * E + (t - 5), (float)s_d[t], kFused);
         }
       for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
-        if ((ran >> st) & 1ull) s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
+        if ((ran >> st) & 1ull) st_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, (uint32_t)min(s_smax[st], 0xFFFF), kFused);
       if (kOnePass && theta0 > 0) {
         const int n = s_ccount;
         if (n > 0) {
@@ -992,8 +1045,24 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           if (n <= kDistK)
             for (int k = tid; k < n; k += kDtThreads)
               if (base + k < (uint32_t)kGCand)
-                s.dist_gcand[(size_t)ea * kGCand + base + k] = make_int2(s_ccell[k], s_cdv[k]);
+                st_ho(s.dist_gcand + (size_t)ea * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused);
         }
+      }
+      if constexpr (kFused) {
+        // every storing wave's stores done, then one arrival per part; the
+        // last to arrive merges (its own loads wait for its add, the other
+        // waves for the barrier after it)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) s_base = atomicAdd(s.dist_pcnt + ea, 1u);
+        __syncthreads();
+        merged = s_base == (uint32_t)S - 1u;
+        if (merged && tid == 0) s.dist_pcnt[ea] = 0;  // zero for the map's next split transform
+      }
+      if (merged) {
+        // the map's bitboard is staged here (every part stages it): a second
+        // cache pass, if the parts' lists overflowed, needs no restaging
+        merge_parts(true);
       }
 #ifdef MC_DIST_STAMPS
       {  // a part (flag bit 52): stage, strips, publish (mode 3 leaves these)
@@ -1008,8 +1077,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       }
 #endif
-      __syncthreads();  // the LDS is reused by the next item
-      continue;
+      if (!merged) {
+        __syncthreads();  // the LDS is reused by the next item
+        continue;
+      }
     }
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
@@ -1066,7 +1137,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         // keep their bound)
         if (cnt > 0)
           for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
-            s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint16_t)min(s_smax[st], 0xFFFF);
+            s.dist_sm[(size_t)ea * kMaxTrack + st] = (uint32_t)min(s_smax[st], 0xFFFF);
         if (tid == 0) {
           reinterpret_cast<int4*>(s.dist_ch + (size_t)ea * 8)[0] = make_int4(cnt, M, 1 << 28, 1 << 28);
           reinterpret_cast<int2*>(s.dist_ch + (size_t)ea * 8)[2] = make_int2(-(1 << 28), -(1 << 28));
@@ -1326,7 +1397,7 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
   // same: 202.3 vs 202.3 us per C5 steady step, profiles/r4/c5_grid/)
   const unsigned g2 = (unsigned)(maps < (size_t)kSplitSlots ? maps : (size_t)kSplitSlots);
   e = launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, g2, 2, full, stream);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || kFused) return e;
   return launch_full(s, pad, 1, pre_out, dist_obs, nullptr, count, g2 < 256 ? g2 : 256, 3, full, stream);
 }
 

@@ -140,15 +140,18 @@ struct State {
   int32_t* dist_cd;
   int32_t* dist_ch;
   // with the cache: per map, an upper bound of max(d) over each 32-column
-  // strip of the extended grid ([B][N][kDistStrips] u16: the strip maxima of
+  // strip of the extended grid ([B][N][kDistStrips] u32: the strip maxima of
   // the last full transform; d only decreases), valid while the cache is
-  uint16_t* dist_sm;
+  // (32-bit words: a split transform's parts hand them over by `sc1` dword
+  // stores, mc_dist.hip)
+  uint32_t* dist_sm;
   // with the cache: the split full transform's per-map partials (mc_dist.hip
   // modes 2 / 3; zero between uses): the best key, the candidate cells
   // published and the candidates [B][N][4 * kDistK] (cell, d)
   unsigned long long* dist_gkey;
   uint32_t* dist_gcnt;
   int2* dist_gcand;
+  uint32_t* dist_pcnt;  // [B][N] parts of a split map done this launch (mode 2 fused; zero between uses)
   // episode record, written when an env reports done (before an auto-reset
   // clears the counters): percent_covered() and _currstep at the end
   double* ep_pc;
