@@ -530,6 +530,10 @@ constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publis
 // the part of a split map that finishes last finalises it inside mode 2
 // (`sc1` hand-off of the partials) instead of a mode-3 launch after it
 constexpr bool kFused = MC_DIST_FUSED != 0;
+#ifndef MC_DIST_XCD  // build knob (A/B): 0 spreads a split map's parts over the XCDs
+#define MC_DIST_XCD 1
+#endif
+constexpr bool kXcdParts = MC_DIST_XCD != 0;
 
 template <int kCL>
 __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
@@ -567,7 +571,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   const int nstrips_all = (RY + kStrip - 1) / kStrip;
   const uint32_t nF = mode >= 2 ? __atomic_load_n(full, __ATOMIC_RELAXED) : 0u;
   const int S = mode >= 2 && nF > 0 ? max(1, min(min(nstrips_all, kMaxParts), (int)(kSplitSlots / nF))) : 1;
-  const uint32_t n_items = mode == 2   ? nF * (uint32_t)S
+  // XCD-aware parts (mode 2, S > 1, a grid of whole XCD rounds): workgroup b
+  // runs on XCD b % 8, so item it = 8 l + x is part l % S of map
+  // 8 (l / S) + x -- every part of a map on one XCD, whose L2 then fetches
+  // the map's tiles once for all of them (each part stages the whole map)
+  const bool xcd = kXcdParts && mode == 2 && S > 1 && (gridDim.x & 7u) == 0u;
+  const uint32_t n_items = mode == 2   ? (xcd ? ((nF + 7u) >> 3) * 8u * (uint32_t)S : nF * (uint32_t)S)
                            : mode == 3 ? (S > 1 ? nF : 0u)
                                        : (list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x);
   const bool strided = mode >= 2 || list != nullptr;
@@ -591,8 +600,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   }
   for (uint32_t it = blockIdx.x; it < n_items; it += (strided ? gridDim.x : n_items)) {
     // modes 2 / 3: the full-list entry (and mode 2's part)
-    const uint32_t fi = mode == 2 ? it / (uint32_t)S : (mode == 3 ? it : 0u);
-    const int part = mode == 2 ? (int)(it - fi * (uint32_t)S) : 0;
+    const uint32_t l = it >> 3;
+    const uint32_t fi = mode == 2 ? (xcd ? (l / (uint32_t)S) * 8u + (it & 7u) : it / (uint32_t)S) : (mode == 3 ? it : 0u);
+    const int part = mode == 2 ? (xcd ? (int)(l % (uint32_t)S) : (int)(it - fi * (uint32_t)S)) : 0;
+    if (fi >= nF && mode == 2) continue;  // (xcd: this XCD's share ran out; uniform per workgroup)
     const uint32_t ea = mode >= 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
     // the strips this workgroup transforms
     const int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
