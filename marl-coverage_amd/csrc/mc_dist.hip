@@ -530,8 +530,10 @@ constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publis
 // the part of a split map that finishes last finalises it inside mode 2
 // (`sc1` hand-off of the partials) instead of a mode-3 launch after it
 constexpr bool kFused = MC_DIST_FUSED != 0;
-#ifndef MC_DIST_XCD  // build knob (A/B): 0 spreads a split map's parts over the XCDs
-#define MC_DIST_XCD 1
+#ifndef MC_DIST_XCD  // build knob (A/B): 1 keeps a split map's parts on one XCD
+// (tried, round 5: the transform launch took 59.0 vs 54.3 us per C5 steady
+// step with the parts spread over the XCDs, profiles/r5/xcd/)
+#define MC_DIST_XCD 0
 #endif
 constexpr bool kXcdParts = MC_DIST_XCD != 0;
 
