@@ -581,6 +581,9 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
   if (C.sub == 0) { L.sc->pen = pen; L.sc->moved = moved; }
 }
 
+#ifndef MC_RPL_SHAPE  // A/B knob: 0 keeps 2 rays per lane per pass for every one-env-per-workgroup shape
+#define MC_RPL_SHAPE 1
+#endif
 #ifndef MC_MOVES_SERIAL  // A/B knob: 1 keeps the serial broadcast rounds (moves) at C5
 #define MC_MOVES_SERIAL 0
 #endif
@@ -1008,10 +1011,10 @@ __device__ __forceinline__ void fan_march(const State& s, const Ctx<NT, EPW, WT>
   }
 }
 
-template <int NT, int EPW, typename WT, int SUK, int KN, int KM = 0>
+template <int NT, int EPW, typename WT, int SUK, int KN, int KM = 0, int RPLX = 0>
 __device__ __forceinline__ void sense(const State& s, const Ctx<NT, EPW, WT>& C) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
-  constexpr int RPL = Ctx<NT, EPW, WT>::RPL;
+  constexpr int RPL = RPLX > 0 ? RPLX : Ctx<NT, EPW, WT>::RPL;
   constexpr int SU = SUK;
   const Lds<WT>& L = C.L;
   const int N = s.N, TW = s.TW, TW2 = TW * TW;
@@ -1385,10 +1388,10 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 }
 
 // sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
-template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0>
+template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0, int RPLX = 0>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
-  sense<NT, EPW, WT, SUK, KN, KM>(s, C);
+  sense<NT, EPW, WT, SUK, KN, KM, RPLX>(s, C);
   __syncthreads();
   STAMP(13);
   if (s.sensor == 0) {
@@ -1417,7 +1420,7 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32, int KM = 0>
+template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32, int KM = 0, int RPLX = 0>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
                                           const int32_t* inj_pos) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
@@ -1494,7 +1497,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI, O32>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
-  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN, KM>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN, KM, RPLX>(s, C, I);
   store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
@@ -1762,8 +1765,17 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   constexpr int KI = CtxT::KI;
   // march steps per batch: the whole march when the shape fixes a short
   // beam_kmax, a quarter of a long one (register pressure)
-  constexpr int SUK = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
+  constexpr int SUK0 = (SH::KM > 0 && SH::KM <= 12) ? SH::KM : (SH::KM > 12 ? (SH::KM + 3) / 4 : 8);
   constexpr int NSM = (SH::N > 0 && SH::N <= 8) ? SH::N : 0;  // compile-time agent count, if small
+  // rays per lane per march pass: 3 where that saves a pass over the
+  // default (C5: 336 rays over 128 lanes, one pass of 3 instead of two of 2)
+  constexpr int RPLK = MC_RPL_SHAPE && SH::N > 0 && SH::NB > 0 && SH::NB < 64 && EPW == 1 &&
+                               (SH::N * SH::NB + 3 * NT - 1) / (3 * NT) < (SH::N * SH::NB + CtxT::RPL * NT - 1) / (CtxT::RPL * NT)
+                           ? 3
+                           : 0;
+  // (3 rays per lane: half the march's batch, the row words of a batch stay
+  // within the register budget)
+  constexpr int SUK = RPLK == 3 ? (SUK0 + 1) / 2 : SUK0;
   // compiled shapes with up to 8 agents: map byte offsets fit 32 bits
   // (launch_env checks; the C5 shape's maps pass 4 GB)
   constexpr bool O32 = SH::N > 0 && SH::N <= 8;
@@ -1959,7 +1971,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       dpre0 = pr[0];
       dprek = pr[1 + k];
     }
-    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM, RPLK>(s, C, I);
     __syncthreads();
     STAMP(5);
     // every lane of the slot computes the reward and done (the same values:
@@ -2043,7 +2055,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, nullptr);  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
@@ -2052,7 +2064,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, reset_req ? inj_pos : nullptr);
     dlist = s.dist && C.sub < N;  // fresh maps: M unknown
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
