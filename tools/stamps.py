@@ -79,7 +79,8 @@ def main():
             continue
         d = s[ok, j] - s[ok, i]
         print(f"  {name:22s} median {np.median(d):8.0f}  p90 {np.percentile(d,90):8.0f}  max {d.max():8d}  n={ok.sum()}")
-    for (i, j), name in [((1, 11), "stage: issue"), ((11, 12), "stage: wait"), ((12, 2), "stage: lds"),
+    for (i, j), name in [((1, 11), "stage: issue"), ((1, 15), "stage: load issue (early moves)"),
+                         ((15, 11), "stage: moves (early moves)"), ((11, 12), "stage: wait"), ((12, 2), "stage: lds"),
                          ((3, 13), "sense: march"), ((13, 4), "sense: gather"),
                          ((4, 14), "merge: mask wait"), ((14, 5), "merge: work+barrier")]:
         ok = (s[:, i] > 0) & (s[:, j] > 0)
