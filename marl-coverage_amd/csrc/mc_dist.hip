@@ -822,42 +822,49 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           if (nrw[q] < RW) firstR = 64 * nrw[q] + __ffsll((unsigned long long)Cb[u * RW + nrw[q]]) - 1;
         }
         const int lc = lastL[q];
-        uint32_t pk[kStrip / 2];
+        // (each 4-column uint2 is stored as soon as it is computed: the
+        // strip's 16 packed pairs never all live in registers at once)
         if (sb == 0u) {
           // no covered cell in the strip: g(j) = min(A + j, B - j), two cells per packed op
           const uint32_t A = (uint32_t)min(c0 - lc, 0xFFFF - kStrip);
           const uint32_t Bd = (uint32_t)min(firstR - c0, 0xFFFF);  // >= 32
           const u16x2 Ap = {(uint16_t)A, (uint16_t)A}, Bp = {(uint16_t)Bd, (uint16_t)Bd};
 #pragma unroll
-          for (int jp = 0; jp < kStrip / 2; ++jp) {
-            const u16x2 cj = {(uint16_t)(2 * jp), (uint16_t)(2 * jp + 1)};
-            const u16x2 g = __builtin_elementwise_min(Ap + cj, Bp - cj);
-            pk[jp] = __builtin_bit_cast(uint32_t, g);
+          for (int k = 0; k < kStrip / 4; ++k) {
+            const u16x2 c0j = {(uint16_t)(4 * k), (uint16_t)(4 * k + 1)};
+            const u16x2 c1j = {(uint16_t)(4 * k + 2), (uint16_t)(4 * k + 3)};
+            const u16x2 g0 = __builtin_elementwise_min(Ap + c0j, Bp - c0j);
+            const u16x2 g1 = __builtin_elementwise_min(Ap + c1j, Bp - c1j);
+            grow[k] = make_uint2(__builtin_bit_cast(uint32_t, g0), __builtin_bit_cast(uint32_t, g1));
           }
         } else if (sb == ~0u) {
 #pragma unroll
-          for (int jp = 0; jp < kStrip / 2; ++jp) pk[jp] = 0u;
+          for (int k = 0; k < kStrip / 4; ++k) grow[k] = make_uint2(0u, 0u);
         } else {
           // g of each cell: nearest covered column at or left of it / at or
           // right of it (inside the strip by bit scans, else the carries)
 #pragma unroll
-          for (int j = 0; j < kStrip; j += 2) {
-            int gg[2];
+          for (int j4 = 0; j4 < kStrip; j4 += 4) {
+            uint32_t pp[2];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
-              const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
-              const int left = le ? c0 + 31 - __clz(le) : lc;
-              const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
-              gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const int j = j4 + 2 * h2;
+              int gg[2];
+#pragma unroll
+              for (int k = 0; k < 2; ++k) {
+                const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
+                const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
+                const int left = le ? c0 + 31 - __clz(le) : lc;
+                const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
+                gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+              }
+              pp[h2] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
             }
-            pk[j >> 1] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
+            grow[j4 >> 2] = make_uint2(pp[0], pp[1]);
           }
           lastL[q] = c0 + 31 - __clz(sb);
         }
         if (sb == ~0u) lastL[q] = c0 + 31;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) grow[k] = make_uint2(pk[2 * k], pk[2 * k + 1]);
       }
       __syncthreads();
       // ---- column pass: column pair p (columns c0 + 2p, c0 + 2p + 1 as the

@@ -584,9 +584,6 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
 #ifndef MC_RPL_SHAPE  // A/B knob: 0 keeps 2 rays per lane per pass for every one-env-per-workgroup shape
 #define MC_RPL_SHAPE 1
 #endif
-#ifndef MC_MOVES_FRONT_PAR  // A/B knob: 0 keeps the every-lane register replay of moves_front (C4: 8 robots)
-#define MC_MOVES_FRONT_PAR 1
-#endif
 #ifndef MC_MOVES_SERIAL  // A/B knob: 1 keeps the serial broadcast rounds (moves) at C5
 #define MC_MOVES_SERIAL 0
 #endif
@@ -713,47 +710,6 @@ __device__ __forceinline__ void moves_front(const State& s, const Ctx<NT, EPW, W
                                             bool tgt_blk, uint32_t txy, int act_own, uint64_t moved,
                                             double pen_unit) {
   const Lds<WT>& L = C.L;
-  if constexpr (!FrontQuad<NS>::ok && NS > 4 && MC_MOVES_FRONT_PAR) {
-    // lane i (< NS) holds robot i: the fixed point of moves_par over the
-    // robots' cells in registers (F.xy: every lane holds every start cell)
-    // and the lanes' own targets read as scalars -- NS compares per lane and
-    // round instead of the every-lane replay of NS x NS compares
-    static_assert(NT == 64 || EPW == 1, "lane i = robot i of the first wave");
-    const int i = C.sub;
-    const bool live = i < NS;
-    const bool acts = live && act_own <= 3;
-    const bool ok0 = acts && !tgt_blk;
-    uint32_t TA[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) TA[j] = (uint32_t)slot_lane(C, (int)txy, j);
-    uint64_t cm = slot_ballot(C, ok0);
-    bool c = ok0;
-    for (int it = 0; it <= NS; ++it) {
-      bool occ = false;
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        const uint32_t pj = ((cm >> j) & 1ull) ? TA[j] : F.xy[j];
-        occ |= (j < i ? pj : F.xy[j]) == txy;
-      }
-      c = ok0 && !occ;
-      const uint64_t nm = slot_ballot(C, c);
-      if (nm == cm) break;
-      cm = nm;
-    }
-    if (live) {
-      const uint32_t xy = c ? txy : F.xy[i < NS ? i : 0];
-      L.x[i] = (int)(xy & 0xFFFFu);
-      L.y[i] = (int)(xy >> 16);
-    }
-    const int fails = __popcll(slot_ballot(C, acts && !c));
-    if (C.sub == 0) {
-      double pen = 0.0;
-      for (int k = 0; k < fails; ++k) pen += pen_unit;  // reward += -collision_penalty per failed move (:203)
-      L.sc->pen = pen;
-      L.sc->moved = moved | cm;
-    }
-    return;
-  }
   // QUAD: every lane holds its quad's robot (sub % NS): its packed target
   // and flags (bit 0 blocked, bit 1 acts) go to the loop by quad_perm
   const int fl = (tgt_blk ? 1 : 0) | (act_own <= 3 ? 2 : 0);
