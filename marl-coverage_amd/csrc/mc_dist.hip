@@ -536,6 +536,31 @@ constexpr bool kFused = MC_DIST_FUSED != 0;
 #define MC_DIST_XCD 0
 #endif
 constexpr bool kXcdParts = MC_DIST_XCD != 0;
+#ifndef MC_DIST_BALANCE  // build knob (A/B): 0 splits a map's strips evenly by count
+#define MC_DIST_BALANCE 1
+#endif
+constexpr bool kBalance = MC_DIST_BALANCE != 0;
+
+// The strips a full transform of map ea runs with the lower bound theta of
+// its new max(d) (bit st; the rest are pruned, dist_kernel_t's strip loop):
+// a strip runs if its last known maximum (State::dist_sm) reaches theta -
+// kDistT or it holds a target cell.  Computed when the map goes to the full
+// list (dist_fast_kernel), before any part of the next launch publishes new
+// strip maxima: every part then splits the same running strips evenly.
+__device__ uint64_t strip_run_mask(const State& s, int pad, uint32_t ea, int theta) {
+  const int RY = s.Lp + 2 * pad, nst = (RY + kStrip - 1) / kStrip;
+  const uint64_t all = nst >= 64 ? ~0ull : low_mask(nst);
+  if (theta <= 0 || nst > kMaxTrack || !s.dist_sm) return all;
+  const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
+  const int tv_lo = min(pp.y - 1, pp.y + pad - s.ego), tv_hi = max(pp.y + 1, pp.y + pad + s.ego);
+  const uint32_t* smb = s.dist_sm + (size_t)ea * kMaxTrack;
+  uint64_t m = 0;
+  for (int st = 0; st < nst; ++st) {
+    const int c0 = st * kStrip;
+    if ((int)smb[st] >= theta - kDistT || (c0 + kStrip > tv_lo && c0 <= tv_hi)) m |= 1ull << st;
+  }
+  return m;
+}
 
 template <int kCL>
 __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
@@ -607,9 +632,28 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     const int part = mode == 2 ? (xcd ? (int)(l % (uint32_t)S) : (int)(it - fi * (uint32_t)S)) : 0;
     if (fi >= nF && mode == 2) continue;  // (xcd: this XCD's share ran out; uniform per workgroup)
     const uint32_t ea = mode >= 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
-    // the strips this workgroup transforms
-    const int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
-    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0;
+    // the strips this workgroup transforms: a contiguous range, the ranges
+    // splitting the map's running strips evenly (strip_run_mask; without a
+    // mask, its strips)
+    int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
+    if (kBalance && mode == 2 && S > 1 && s.dist_rmask) {
+      const uint64_t rm = s.dist_rmask[ea];
+      if (rm) {
+        const int R = __popcll(rm);
+        // the first strip of the part holding running strip of rank p R / S
+        auto bound = [&](int p) -> int {
+          if (p == 0) return 0;
+          const int r = p * R / S;
+          if (p >= S || r >= R) return nstrips_all;
+          uint64_t m = rm;
+          for (int k = 0; k < r; ++k) m &= m - 1ull;
+          return __ffsll((unsigned long long)m) - 1;
+        };
+        st_lo = bound(part);
+        st_hi = bound(part + 1);
+      }
+    }
+    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0, tsa = 0, tsb = 0;
     DSTAMP(ts0);
     const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
     const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
@@ -721,51 +765,73 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         uint8_t* crow = reinterpret_cast<uint8_t*>(G);
         uint64_t* crw = reinterpret_cast<uint64_t*>(G);
         const int RWm = (s.TC + 7) >> 3;  // u64 words per map row
-        for (int q = tid; q < s.TR * RWm; q += kDtThreads) {
-          const int ti = q / RWm, w = q - ti * RWm;
-          uint32_t lo[8], hi[8];  // tile j's dwords (rows 0-3, rows 4-7)
+        const int nq = s.TR * RWm;
+        // two items per thread per round, every load of both issued first
+        // (a 514-row map has 585 items: one round of load latency, not two)
+        for (int q0 = tid; q0 < nq; q0 += 2 * kDtThreads) {
+          uint32_t lo[2][8], hi[2][8];  // tile j's dwords (rows 0-3, rows 4-7)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int tj = 8 * w + j;
-            const uint64_t t = tj < s.TC ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
-            lo[j] = (uint32_t)t;
-            hi[j] = (uint32_t)(t >> 32);
+          for (int k = 0; k < 2; ++k) {
+            const int q = q0 + k * kDtThreads;
+            const int ti = q / RWm, w = q - ti * RWm;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int tj = 8 * w + j;
+              const uint64_t t = (q < nq && tj < s.TC) ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
+              lo[k][j] = (uint32_t)t;
+              hi[k][j] = (uint32_t)(t >> 32);
+            }
           }
-          const int nr = min(8, s.Wp - 8 * ti);
 #pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            if (r >= nr) break;
-            const uint32_t* src = r < 4 ? lo : hi;
-            const uint32_t b = (uint32_t)(r & 3);
-            // byte b of src[j]: pairs (j, j + 1) -> bytes 0, 1 of a dword,
-            // then two such pairs -> 4 bytes
-            const uint32_t sel2 = b | ((4u + b) << 8) | 0x0C0C0000u;
-            const uint32_t p01 = __builtin_amdgcn_perm(src[1], src[0], sel2);
-            const uint32_t p23 = __builtin_amdgcn_perm(src[3], src[2], sel2);
-            const uint32_t p45 = __builtin_amdgcn_perm(src[5], src[4], sel2);
-            const uint32_t p67 = __builtin_amdgcn_perm(src[7], src[6], sel2);
-            const uint32_t wlo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
-            const uint32_t whi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
-            crw[(size_t)(8 * ti + r) * RWm + w] = (uint64_t)wlo | ((uint64_t)whi << 32);
+          for (int k = 0; k < 2; ++k) {
+            const int q = q0 + k * kDtThreads;
+            if (q >= nq) break;
+            const int ti = q / RWm, w = q - ti * RWm;
+            const int nr = min(8, s.Wp - 8 * ti);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              if (r >= nr) break;
+              const uint32_t* src = r < 4 ? lo[k] : hi[k];
+              const uint32_t b = (uint32_t)(r & 3);
+              // byte b of src[j]: pairs (j, j + 1) -> bytes 0, 1 of a dword,
+              // then two such pairs -> 4 bytes
+              const uint32_t sel2 = b | ((4u + b) << 8) | 0x0C0C0000u;
+              const uint32_t p01 = __builtin_amdgcn_perm(src[1], src[0], sel2);
+              const uint32_t p23 = __builtin_amdgcn_perm(src[3], src[2], sel2);
+              const uint32_t p45 = __builtin_amdgcn_perm(src[5], src[4], sel2);
+              const uint32_t p67 = __builtin_amdgcn_perm(src[7], src[6], sel2);
+              const uint32_t wlo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+              const uint32_t whi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
+              crw[(size_t)(8 * ti + r) * RWm + w] = (uint64_t)wlo | ((uint64_t)whi << 32);
+            }
           }
         }
+        DSTAMP(tsa);
         __syncthreads();
+        DSTAMP(tsb);
         const uint64_t* cw = reinterpret_cast<const uint64_t*>(crow);
         int any = 0;
-        for (int u = tid; u < RX; u += kDtThreads) {  // a row per thread
+        // a (row, word) item per thread and round (RX rows of RW words: 532
+        // rows would leave 20 threads two whole rows)
+        const int du = kDtThreads / RW, dw = kDtThreads - du * RW;
+        int u = tid / RW, w = tid - u * RW;
+        for (int idx = tid; idx < RX * RW; idx += kDtThreads) {
           const int X = u - pad;
-          const bool in = X >= 0 && X < s.Wp;
-          for (int w = 0; w < RW; ++w) {
-            uint64_t c = 0;
-            if (in) {  // map columns [64 w - pad, 64 w - pad + 64)
-              const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
-              const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
-              const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
-              c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
-            }
-            c &= (w == RW - 1) ? last : ~0ull;
-            Cb[u * RW + w] = c;
-            any |= c != 0;
+          uint64_t c = 0;
+          if (X >= 0 && X < s.Wp) {  // map columns [64 w - pad, 64 w - pad + 64)
+            const int off = 64 * w - pad, ws = off >> 6, sh = off & 63;  // floor
+            const uint64_t a0 = (ws >= 0 && ws < RWm) ? cw[X * RWm + ws] : 0ull;
+            const uint64_t a1 = (ws + 1 >= 0 && ws + 1 < RWm) ? cw[X * RWm + ws + 1] : 0ull;
+            c = sh ? ((a0 >> sh) | (a1 << (64 - sh))) : a0;
+          }
+          c &= (w == RW - 1) ? last : ~0ull;
+          Cb[idx] = c;
+          any |= c != 0;
+          w += dw;
+          u += du;
+          if (w >= RW) {
+            w -= RW;
+            ++u;
           }
         }
         if (any) s_cov = 1;
@@ -1094,6 +1160,15 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
             return d < 0xFFFFull ? d : 0xFFFFull;
           };
           s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, tp) << 32) | (1ull << 52);
+          // per part (tools/dist_stamps.py allocates B*16 + 8192 entries):
+          // stage, strips, publish, strips run, S, merged
+          if (it < 4096u)
+            s.stamps[(size_t)s.B * 16u + 8192u + it] =
+                f16(ts0, tsa) | (f16(tsa, tsb) << 16) | (f16(tsb, ts1) << 32) | (1ull << 59);
+          if (it < 4096u)
+            s.stamps[(size_t)s.B * 16u + it] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, tp) << 32) |
+                                               ((uint64_t)min(__popcll(ran), 63) << 48) | ((uint64_t)S << 54) |
+                                               ((uint64_t)merged << 58) | (1ull << 59);
         }
       }
 #endif
@@ -1185,8 +1260,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, ts3) << 32) | dflags |
                      (fast ? 1ull << 48 : 0ull) | (ff << 51);
     }
+    if (tid == 0 && s.stamps && mode == 2 && merged && it < 4096u) {  // the merged part: publish end -> done
+      const uint64_t d = (ts3 - ts0) >> 4;
+      s.stamps[(size_t)s.B * 16u + 4096u + it] = (d < 0xFFFFFFull ? d : 0xFFFFFFull) | (1ull << 59);
+    }
 #else
-    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)tsf; (void)dflags;
+    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)tsf; (void)dflags; (void)tsa; (void)tsb;
 #endif
     __syncthreads();  // the LDS is reused by the next item
   }
@@ -1275,6 +1354,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   // straight to the full list), then the workgroup tries the cache of each
   // map that has one
   auto to_full = [&](uint32_t ea, uint32_t theta) {  // (one thread)
+    if (s.dist_rmask) s.dist_rmask[ea] = strip_run_mask(s, pad, ea, (int)theta);
     const uint32_t k = atomicAdd(&s_nf, 1u);
     if (k < (uint32_t)kFastBuf) s_fl[k] = make_uint2(ea, theta);
     else reinterpret_cast<uint2*>(full + 8)[atomicAdd(full, 1u)] = make_uint2(ea, theta);

@@ -152,6 +152,10 @@ struct State {
   uint32_t* dist_gcnt;
   int2* dist_gcand;
   uint32_t* dist_pcnt;  // [B][N] parts of a split map done this launch (mode 2 fused; zero between uses)
+  // [B][N] the strips a listed map's split transform runs (bit st: not
+  // pruned; mc_dist.hip strip_run_mask), written when the map goes to the full
+  // list, read by every part of the next launch to balance the parts
+  unsigned long long* dist_rmask;
   // episode record, written when an env reports done (before an auto-reset
   // clears the counters): percent_covered() and _currstep at the end
   double* ep_pc;

@@ -188,3 +188,97 @@ def test_c5_bench_shape_full_size(torch_cuda):
                                            inv_every=10, dist_every=3)
     assert listed > 0 and cached > 0, (listed, cached)
     assert int(env.get_state(_lib.FIELD_CURRSTEP).min()) == 30
+
+
+def run_deep(torch, cfgname, maxsteps, steps, sample, variant, state_every, dist_every=0):
+    """Deep-episode parity: the sample is tracked by the
+    oracle from the reset through ``steps`` bench steps, so the accumulated
+    state -- every free / obstacle / union mark since the reset, the counters
+    and positions -- is checked, not a transition from device state.  Obs,
+    done and positions every step; the full maps every ``state_every`` steps
+    and at the end (unpacking 16 x 512 x 512 planes per step would dominate).
+
+    dist_reward configs: the oracle's distance term is stateless (observe()
+    recomputes the map from the free plane, dec_grid_rl.py:222-223,239-240),
+    so the tracker runs with it off between checkpoints (obs layers 0..2
+    compared, reward not) and on at every ``dist_every``-th step and the last
+    25 steps (reward with the float32 distance terms, the float distance obs
+    layer)."""
+    from marlcov import streams
+    from oracle.cpu_ref import DecGridRLRef
+    env, cfg, seeds = bench_env(cfgname, maxsteps)
+    assert env.kernel_variant() == variant, env.kernel_variant()
+    N = env.num_agents
+    dist = bool(cfg.get("dist_reward"))
+    sel = torch.tensor(sample, device=env.device)
+    env.reset()
+    st = device_state(env, sample)
+    refs = {}
+    for b in sample:
+        g = int(st["env_grid"][b])
+        grid = np.where(st["neg"][g] == 1, -1.0, np.where(st["pos_plane"][g] == 1, 1.0, 0.0))
+        np.random.seed(0)
+        ref = DecGridRLRef([grid[1:-1, 1:-1]], cfg)
+        ref.reset(False, None, positions=[tuple(q) for q in st["pos"][b]])
+        refs[b] = ref
+    resets = 0
+    for t in range(steps):
+        a = env.random_actions(seeds["action_seed"], t)
+        obs, rew, done = env.step(a)
+        full = dist and ((dist_every and t % dist_every == 0) or t >= steps - 25)
+        o_dev = obs.index_select(0, sel).cpu().numpy().astype(np.float64)
+        if full:
+            o_dev[:, :, 3] = env.dist_obs.index_select(0, sel).cpu().numpy().astype(np.float64)
+        rew_h, done_h = rew.index_select(0, sel).cpu().numpy(), done.index_select(0, sel).cpu().numpy()
+        a_h = a.index_select(0, sel).cpu().numpy()
+        check_state = t % state_every == state_every - 1 or t == steps - 1
+        st = device_state(env, sample) if check_state else None
+        from marlcov import _lib
+        pos = env.get_state(_lib.FIELD_POS).index_select(0, sel).cpu().numpy()
+        for k, b in enumerate(sample):
+            ref = refs[b]
+            if dist:
+                ref._dist_r = 1 if full else 0
+            o, r, d = ref.step(a_h[k].astype(np.int64))
+            tag = f"{cfgname} deep t={t + 1} env {b}"
+            if full or not dist:
+                assert float(r) == rew_h[k], (tag, float(r), rew_h[k])
+            assert bool(d) == bool(done_h[k]), tag
+            if d:
+                resets += 1
+                ep = int(env.get_state(_lib.FIELD_EPISODE)[b].item())
+                want = streams.start_cells(seeds["env_seed"], b, ep, ref._grid, N)
+                np.testing.assert_array_equal(pos[k], want, err_msg=tag + " start cells vs host Philox")
+                o, _ = ref.reset(False, None, positions=[tuple(q) for q in pos[k]])
+                if dist and not full:
+                    o = o[:, :3]
+            np.testing.assert_array_equal(o_dev[k][:, :o.shape[1]], o, err_msg=tag + " obs")
+            np.testing.assert_array_equal(pos[k, :, 0], ref._xinds, err_msg=tag + " x")
+            np.testing.assert_array_equal(pos[k, :, 1], ref._yinds, err_msg=tag + " y")
+            if check_state:
+                compare_env(st, b, ref, tag)
+    env.check()
+    return env, resets
+
+
+def test_c2_bench_shape_deep_episode(torch_cuda):
+    """C2 at the bench's own episode length (maxsteps 1000): 4 envs tracked by
+    the oracle from the reset through 1,040 steps -- the whole first episode,
+    the auto-reset at step 1000 inside the kernel and 40 steps of the next."""
+    env, resets = run_deep(torch_cuda, "c2", 1000, 1040, [5, 1234, 2222, 4090], "env_kernel<64,2,u32,C2>",
+                           state_every=50)
+    assert resets >= 4
+
+
+def test_c4_bench_shape_deep_episode(torch_cuda):
+    """C4 at 8,192 envs: 1 env tracked by the oracle from the reset through 400
+    steps (the fan march's marks accumulated over the episode)."""
+    run_deep(torch_cuda, "c4", 1000, 400, [4444], "env_kernel<256,1,u64,C4> +fan(64/2)", state_every=50)
+
+
+def test_c5_bench_shape_deep_episode(torch_cuda):
+    """C5 at 8,192 envs: 1 env tracked by the oracle from the reset through 625
+    steps -- the accumulated maps under which test_c5_cache_steady_state_
+    matches_oracle starts -- with the distance terms checked every 25 steps and
+    in the last 25 (the top-cell cache's steady state)."""
+    run_deep(torch_cuda, "c5", 2000, 625, [3001], "env_kernel<128,1,u32,C5>", state_every=100, dist_every=25)

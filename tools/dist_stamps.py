@@ -45,14 +45,21 @@ def main():
     env.reset()
     for t in range(args.warmup):
         env.step(env.random_actions(7, t))
-    st = torch.zeros((B, 16), dtype=torch.int64, device=env.device)
+    st = torch.zeros((B * 16 + 12288,), dtype=torch.int64, device=env.device)  # + per-part records
     _lib.check(env.lib.mc_debug_stamps(env._h, st.data_ptr()), "stamps")
     env.step(env.random_actions(7, args.warmup))
     torch.cuda.synchronize()
     listed = int(env.get_state(_lib.FIELD_DIST_LISTED).item())
     served = int(env.get_state(_lib.FIELD_DIST_CACHED).item())
-    s = st.cpu().numpy().reshape(-1).astype(np.uint64)
+    allst = st.cpu().numpy().reshape(-1).astype(np.uint64)
+    s = allst[:B * 16]
     s = s[s != 0]
+    parts = allst[B * 16:B * 16 + 4096]
+    parts = parts[parts != 0]
+    sub = allst[B * 16 + 8192:]
+    sub = sub[sub != 0]
+    merged_tot = allst[B * 16 + 4096:B * 16 + 8192]
+    merged_tot = (merged_tot[merged_tot != 0] & np.uint64(0xFFFFFF)).astype(np.int64) * 16
     print(f"step {args.warmup + 1}: listed {listed}, cache served {served}, stamped {len(s)}")
     fast = (s >> np.uint64(48)) & np.uint64(1)
     kept = (s >> np.uint64(49)) & np.uint64(1)
@@ -75,6 +82,25 @@ def main():
         row = "  ".join(f"{lab} med {np.median(p[m]):8.0f} p90 {np.percentile(p[m], 90):8.0f} max {p[m].max():8d}"
                         for lab, p in zip(labs, ph) if lab)
         print(f"  {name:22s} n={m.sum():5d}  {row}")
+    if len(parts):
+        f = [((parts >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
+        nrun = ((parts >> np.uint64(48)) & np.uint64(63)).astype(np.int64)
+        S = ((parts >> np.uint64(54)) & np.uint64(15)).astype(np.int64)
+        tot = f[0] + f[1] + f[2]
+        print(f"  parts: n={len(parts)}  S values {sorted(set(S.tolist()))}  part total med {np.median(tot):.0f} "
+              f"p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
+        for k in sorted(set(nrun.tolist())):
+            m = nrun == k
+            print(f"    strips run {k:2d}: n={m.sum():4d}  stage med {np.median(f[0][m]):7.0f}  strips med "
+                  f"{np.median(f[1][m]):7.0f} max {f[1][m].max():7d}  publish med {np.median(f[2][m]):7.0f} "
+                  f"max {f[2][m].max():7d}")
+        if len(sub):
+            g = [((sub >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
+            print("    stage split: " + "  ".join(f"{lab} med {np.median(x):7.0f} p90 {np.percentile(x, 90):7.0f}"
+                                              for lab, x in zip(("loads+transpose", "barrier", "extend rows"), g)))
+        if len(merged_tot):
+            print(f"  merged parts (start -> done): n={len(merged_tot)} med {np.median(merged_tot):.0f} "
+                  f"p90 {np.percentile(merged_tot, 90):.0f} max {merged_tot.max()}")
 
 
 if __name__ == "__main__":
