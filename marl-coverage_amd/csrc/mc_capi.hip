@@ -77,7 +77,7 @@ struct Env {
   float* dist_pre = nullptr;  // dist_reward: [B][N][8] (library-owned)
   float* dist_obs = nullptr;  // dist_reward: caller's float32 [B][N][E][E]
   double* mini_obs = nullptr; // mini_map_rad: caller's float64 [B][N][2][E][E]
-  uint32_t* dist_list = nullptr;  // dist_reward: count, workgroups done, last count, cache hits, last hits + [B*N] maps (full transform)
+  uint32_t* dist_list = nullptr;  // dist_reward: (unused), workgroups done, last count, cache hits, last hits + the shards' maps (full transform)
   uint32_t* dist_full = nullptr;  // with the cache: the split transform's list (mc_dist.hip mode 2)
   bool dist_pre_stale = true;  // dist_pre does not describe the current maps
   bool beams_set = false;
@@ -402,9 +402,11 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->s.dist_pre = E->dist_pre;
     // (M, witness) per map, M = -1 (unknown) until a full transform; the
     // work list of the full transform and its count
-    void *mw = nullptr, *lq = nullptr, *tq = nullptr;
+    void *mw = nullptr, *lq = nullptr, *tq = nullptr, *sh = nullptr;
+    const size_t cap = (size_t)((s.B + mc::kListShards - 1) / mc::kListShards) * s.N;  // entries per shard
     if (dev_alloc(E, &mw, (size_t)s.B * s.N * 8) != MC_OK ||
-        dev_alloc(E, &lq, ((size_t)s.B * s.N + 5) * 4) != MC_OK || dev_alloc(E, &tq, 32) != MC_OK ||
+        dev_alloc(E, &lq, (mc::kListShards * cap + 5) * 4) != MC_OK || dev_alloc(E, &tq, 32) != MC_OK ||
+        dev_alloc(E, &sh, mc::kListShards * mc::kShardStride * 4) != MC_OK ||
         hipMemset(mw, 0xFF, (size_t)s.B * s.N * 8) != hipSuccess) {
       std::string msg = g_err;
       mc_destroy(E);
@@ -413,6 +415,8 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     E->s.dist_mw = (int32_t*)mw;
     E->dist_list = (uint32_t*)lq;
     E->s.dist_cnt = E->dist_list;
+    E->s.dist_shc = (uint32_t*)sh;
+    E->s.dist_cap = (uint32_t)cap;
     E->s.dist_tot = (unsigned long long*)tq;
     // the top-cell cache (mc_dist.hip), off with map sharing (other agents'
     // maps add cells outside the agent's own sensing windows) or

@@ -238,6 +238,26 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
   return v;
 }
+
+// The env kernel's work list: kListShards shards of s.dist_cap entries
+// (State::dist_shc), read as one list of pre[kListShards] entries in shard
+// order.  The counts were written by an earlier launch: plain loads.
+struct ListView {
+  uint32_t pre[kListShards + 1];  // entries before shard k
+};
+__device__ __forceinline__ ListView list_view(const State& s) {
+  ListView v;
+  v.pre[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kListShards; ++k) v.pre[k + 1] = v.pre[k] + s.dist_shc[k * kShardStride];
+  return v;
+}
+__device__ __forceinline__ uint32_t list_entry(const State& s, const ListView& v, const uint32_t* list, uint32_t i) {
+  uint32_t off = i;
+#pragma unroll
+  for (int k = 1; k < kListShards; ++k) off = i >= v.pre[k] ? (uint32_t)k * s.dist_cap + (i - v.pre[k]) : off;
+  return list[off];
+}
 }  // namespace
 
 // rows per column chunk: the instantiation (8, 17 or 26) whose kCh chunks
@@ -596,6 +616,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // of a device work list (a fixed grid strides over *count entries: the
   // count is uniform, so every wave reaches the end)
   const int nstrips_all = (RY + kStrip - 1) / kStrip;
+  uint64_t tk = 0;  // (diagnostic) the workgroup's start
+  DSTAMP(tk);
   const uint32_t nF = mode >= 2 ? __atomic_load_n(full, __ATOMIC_RELAXED) : 0u;
   const int S = mode >= 2 && nF > 0 ? max(1, min(min(nstrips_all, kMaxParts), (int)(kSplitSlots / nF))) : 1;
   // XCD-aware parts (mode 2, S > 1, a grid of whole XCD rounds): workgroup b
@@ -603,9 +625,12 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   // 8 (l / S) + x -- every part of a map on one XCD, whose L2 then fetches
   // the map's tiles once for all of them (each part stages the whole map)
   const bool xcd = kXcdParts && mode == 2 && S > 1 && (gridDim.x & 7u) == 0u;
+  ListView lv;
+  lv.pre[kListShards] = 0;
+  if (list && mode < 2) lv = list_view(s);
   const uint32_t n_items = mode == 2   ? (xcd ? ((nF + 7u) >> 3) * 8u * (uint32_t)S : nF * (uint32_t)S)
                            : mode == 3 ? (S > 1 ? nF : 0u)
-                                       : (list ? __atomic_load_n(count, __ATOMIC_RELAXED) : (uint32_t)gridDim.x);
+                                       : (list ? lv.pre[kListShards] : (uint32_t)gridDim.x);
   const bool strided = mode >= 2 || list != nullptr;
   if (mode == 2 && blockIdx.x == 0 && tid == 0) {
     // mode 1 has drained the list: its counters for the diagnostics
@@ -614,15 +639,19 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // workgroup, all on one address) and empty for the next step's env
     // kernel (no per-workgroup done counters in modes 1 / 2; the env kernel
     // empties the full list)
-    count[2] = count[0];
-    count[4] = count[0] - nF;
+    uint32_t nl = 0;
+    for (int k = 0; k < kListShards; ++k) {
+      nl += s.dist_shc[k * kShardStride];
+      s.dist_shc[k * kShardStride] = 0;
+    }
+    count[2] = nl;
+    count[4] = nl - nF;
     if (s.dist_tot) {  // MC_FIELD_DIST_TOTALS (one thread, stream-ordered)
-      s.dist_tot[0] += count[0];
-      s.dist_tot[1] += count[0] - nF;
+      s.dist_tot[0] += nl;
+      s.dist_tot[1] += nl - nF;
       s.dist_tot[2] += nF;
       s.dist_tot[3] += 1ull;
     }
-    count[0] = 0;
     count[3] = 0;
   }
   for (uint32_t it = blockIdx.x; it < n_items; it += (strided ? gridDim.x : n_items)) {
@@ -631,7 +660,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     const uint32_t fi = mode == 2 ? (xcd ? (l / (uint32_t)S) * 8u + (it & 7u) : it / (uint32_t)S) : (mode == 3 ? it : 0u);
     const int part = mode == 2 ? (xcd ? (int)(l % (uint32_t)S) : (int)(it - fi * (uint32_t)S)) : 0;
     if (fi >= nF && mode == 2) continue;  // (xcd: this XCD's share ran out; uniform per workgroup)
-    const uint32_t ea = mode >= 2 ? full[8 + 2 * fi] : (list ? list[it] : it);
+    const uint32_t ea = mode >= 2 ? full[8 + 2 * fi] : (list ? list_entry(s, lv, list, it) : it);
     // the strips this workgroup transforms: a contiguous range, the ranges
     // splitting the map's running strips evenly (strip_run_mask; without a
     // mask, its strips)
@@ -1162,6 +1191,11 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, tp) << 32) | (1ull << 52);
           // per part (tools/dist_stamps.py allocates B*16 + 8192 entries):
           // stage, strips, publish, strips run, S, merged
+          if (it < 4096u) {  // absolute: workgroup start, item start, part end (merged: below)
+            s.stamps[(size_t)s.B * 16u + 12288u + it] = ts0;
+            s.stamps[(size_t)s.B * 16u + 16384u + it] = tp;
+            s.stamps[(size_t)s.B * 16u + 20480u + it] = tk;
+          }
           if (it < 4096u)
             s.stamps[(size_t)s.B * 16u + 8192u + it] =
                 f16(ts0, tsa) | (f16(tsa, tsb) << 16) | (f16(tsb, ts1) << 32) | (1ull << 59);
@@ -1263,14 +1297,15 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     if (tid == 0 && s.stamps && mode == 2 && merged && it < 4096u) {  // the merged part: publish end -> done
       const uint64_t d = (ts3 - ts0) >> 4;
       s.stamps[(size_t)s.B * 16u + 4096u + it] = (d < 0xFFFFFFull ? d : 0xFFFFFFull) | (1ull << 59);
+      s.stamps[(size_t)s.B * 16u + 16384u + it] = ts3;
     }
 #else
-    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)tsf; (void)dflags; (void)tsa; (void)tsb;
+    (void)ts0; (void)ts1; (void)ts2; (void)ts3; (void)tsf; (void)dflags; (void)tsa; (void)tsb; (void)tk;
 #endif
     __syncthreads();  // the LDS is reused by the next item
   }
-  // count[0] = entries, count[1] = workgroups done: the last workgroup to
-  // finish zeroes both for the next step's env kernel (every workgroup has
+  // the shards' counts (State::dist_shc) = entries, count[1] = workgroups
+  // done: the last workgroup to finish zeroes them for the next step's env kernel (every workgroup has
   // read the entry count before it counts itself done; no memset launch per
   // step) and keeps the entry count in count[2] (MC_FIELD_DIST_LISTED); the
   // cache hits count[3] go to count[4] the same way (MC_FIELD_DIST_CACHED)
@@ -1284,7 +1319,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     } else {
       __threadfence();
       if (atomicAdd(cnt + 1, 1u) == gridDim.x - 1) {
-        const uint32_t nl = atomicExch(cnt, 0u), nh = atomicExch(cnt + 3, 0u);
+        uint32_t nl = 0;
+        for (int k = 0; k < kListShards; ++k) nl += atomicExch(s.dist_shc + k * kShardStride, 0u);
+        const uint32_t nh = atomicExch(cnt + 3, 0u);
         atomicExch(cnt + 2, nl);
         atomicExch(cnt + 4, nh);
         atomicExch(cnt + 1, 0u);
@@ -1345,7 +1382,8 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
   __shared__ uint32_t s_span[6 * kSpan];
   const int tid = threadIdx.x;
   const int T = 5 + s.E * s.E;
-  const uint32_t n_items = __atomic_load_n(count, __ATOMIC_RELAXED);
+  const ListView lv = list_view(s);
+  const uint32_t n_items = lv.pre[kListShards];
   uint64_t tk0 = 0;
   DSTAMP(tk0);
   if (tid == 0) s_nf = 0;
@@ -1366,7 +1404,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
     if (tid == 0) s_nc = 0;
     __syncthreads();
     for (uint32_t i = c0 + tid; i < c1; i += kFastThreads) {
-      const uint32_t ea = list[i];
+      const uint32_t ea = list_entry(s, lv, list, i);
       if (s.dist_ch[(size_t)ea * 8] > 0) s_cl[atomicAdd(&s_nc, 1u)] = ea;
       else to_full(ea, 0u);
     }

@@ -584,6 +584,9 @@ __device__ __forceinline__ void moves(const State& s, const Ctx<NT, EPW, WT>& C,
 #ifndef MC_RPL_SHAPE  // A/B knob: 0 keeps 2 rays per lane per pass for every one-env-per-workgroup shape
 #define MC_RPL_SHAPE 1
 #endif
+#ifndef MC_ABL  // diagnostic ablations (timing only, results wrong): 1 no dist_window, 2 no dist rows in
+#define MC_ABL 0  // merge, 3 no overlap dedup in merge, 4 no obs, 5 no sensing march
+#endif
 #ifndef MC_MOVES_SERIAL  // A/B knob: 1 keeps the serial broadcast rounds (moves) at C5
 #define MC_MOVES_SERIAL 0
 #endif
@@ -1193,12 +1196,19 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
   // (ds_bpermute) and reads only those agents' marks -- usually none, where
   // the loop over every lower agent ran up to N - 1 readlane rounds per item
   uint64_t ovj = 0;
-  if constexpr (NS == 0 && EPW == 1) {
+  if constexpr (NS == 0 && EPW == 1 && MC_ABL != 3) {
+    // branch-free: |dx| < TW as one unsigned compare, the b < j condition as
+    // one mask at the end (per-b lane conditions became exec-mask branches
+    // with spilled SGPR masks)
+    const uint32_t span = (uint32_t)(2 * TW - 1);
+    uint32_t lo = 0, hi = 0;
     for (int b = 0; b < s.N - 1; ++b) {  // uniform trip count (unrolled when N is compiled in)
       const int bxb = rdlane(abx, b), byb = rdlane(aby, b);
-      const bool ov = b < jw && abs(abx - bxb) < TW && abs(aby - byb) < TW;
-      ovj |= ov ? (1ull << b) : 0ull;
+      const uint32_t ov = (uint32_t)((uint32_t)(abx - bxb + TW - 1) < span) & (uint32_t)((uint32_t)(aby - byb + TW - 1) < span);
+      if (b < 32) lo |= ov << b;
+      else hi |= ov << (b - 32);
     }
+    ovj = ((uint64_t)hi << 32 | lo) & (jw >= 64 ? ~0ull : ((1ull << jw) - 1ull));
   }
   // (fetched with every lane active: ds_bpermute reads 0 from inactive lanes)
   uint64_t ova[KI];
@@ -1231,7 +1241,7 @@ __device__ __forceinline__ void merge(const State& s, const Ctx<NT, EPW, WT>& C,
       I.no[k] = op & ~o0;
       L.fold[idx] = f0 | fp;
       L.oold[idx] = o0 | op;
-      if (s.dist) {
+      if (s.dist && MC_ABL != 2) {
         // dist_reward: the post-step free tile's 8 rows into the (dead)
         // mark-row plane, for dist_window (byte tj of block rows 8 ti ..)
         uint8_t* rb = reinterpret_cast<uint8_t*>(L.fpr);
@@ -1359,6 +1369,118 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
   }
 }
 
+// The same terms, one lane per (agent, target row): every target of the
+// agent lies in the rows px - ego .. px + ego (the crop) or px - pad - 1 ..
+// px - pad + 1 (the end cells at the quirk index), so N * 6 items at C5 where
+// the loop above ran N * (5 + E * E).  A lane grows the set of its row's
+// cells within L1 distance D of a covered block cell, D = 0, 1, ..:
+//   S_D = S_{D-1} | S_{D-1} << 1 | S_{D-1} >> 1 | row(lx - D) | row(lx + D)
+// (cells of row lx within D of a covered cell of rows lx - D' .. lx + D'), and
+// a cell's d is the first D whose S_D holds it, recorded in five bit planes.
+// It stops once every target of the row is reached or D passes the largest
+// bound b of its targets (d > b: the agent goes to the full transform, as
+// above).  Rows outside the block read as empty, columns are the block's:
+// the same block-restricted distance as the row scans above.
+// Tried, round 5 (profiles/r5/win/): C5 steady env kernel 83.6 us against
+// 81.7 with the loop above -- a lane's serial D steps, extractions and float
+// divisions cost more than the 4 balanced passes of (agent, target) items.
+#ifndef MC_DIST_WIN  // build knob (A/B): 1 runs dist_window_rows
+#define MC_DIST_WIN 0
+#endif
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void dist_window_rows(const State& s, const Ctx<NT, EPW, WT>& C, uint64_t skip) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  const Lds<WT>& L = C.L;
+  const int N = s.N, E = s.E, ego = s.ego, pad = s.pad, RB = 8 * s.TW;
+  const WT cols = sizeof(WT) == 8 && RB >= 64 ? ~(WT)0 : (WT)(((uint64_t)1 << RB) - 1);  // the block's columns
+  const int r_lo = min(-ego, -pad - 1), r_hi = max(ego, -pad + 1), NR = r_hi - r_lo + 1;
+  float* pre = const_cast<float*>(s.dist_pre);
+  for (int idx = C.sub; idx < N * NR; idx += LPE) {
+    const int a = idx / NR, rr = r_lo + (idx - a * NR);
+    const int M = L.dm[a];
+    if (((skip >> a) & 1ull) || M < 0) continue;
+    const int px = L.x[a], py = L.y[a];
+    const int lx = px + rr - 8 * L.bx[a];  // this lane's block row
+    const int ly0 = py - 8 * L.by[a];      // the robot's block column
+    const bool crop = rr >= -ego && rr <= ego;
+    const int er = rr + pad;               // end cells: rows -pad - 1 .. -pad + 1 (t 3, 0 / 2 / 4, 1)
+    const bool endr = er >= -1 && er <= 1;
+    // the row's targets: the crop's E cells (columns ly0 - ego ..), the end
+    // cells (column ly0 - pad, and ly0 - pad +- 1 in row -pad); bound
+    // b = distance to the block's edge + 1 (<= 0: outside the block)
+    const int brow = min(lx, RB - 1 - lx) + 1;
+    int bmax = -1;
+    WT tmask = 0;
+    auto add_target = [&](int ly) {
+      const int b = min(brow, min(ly, RB - 1 - ly) + 1);
+      bmax = max(bmax, b);
+      if (b > 0) tmask |= (WT)1 << ly;
+    };
+    if (crop)
+      for (int c = 0; c < E; ++c) add_target(ly0 - ego + c);
+    if (endr) {
+      add_target(ly0 - pad);
+      if (er == 0) {
+        add_target(ly0 - pad + 1);
+        add_target(ly0 - pad - 1);
+      }
+    }
+    // grow S while some target is unreached and D <= bmax
+    WT S = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;  // (b <= 32: D < 64)
+    if (bmax > 0) {
+      S = L.fpr[row_word<WT>(s, a, lx)] & cols;
+      for (int D = 1; D <= bmax && (S & tmask) != tmask; ++D) {
+        WT n = S | (S << 1) | (S >> 1);
+        if (lx - D >= 0) n |= L.fpr[row_word<WT>(s, a, lx - D)];
+        if (lx + D < RB) n |= L.fpr[row_word<WT>(s, a, lx + D)];
+        n &= cols;
+        const WT nb = n & ~S;
+        p0 |= (D & 1) ? nb : (WT)0;
+        p1 |= (D & 2) ? nb : (WT)0;
+        p2 |= (D & 4) ? nb : (WT)0;
+        p3 |= (D & 8) ? nb : (WT)0;
+        p4 |= (D & 16) ? nb : (WT)0;
+        p5 |= (D & 32) ? nb : (WT)0;
+        S = n;
+      }
+    }
+    // d of block column ly (b + 1 when unreached)
+    auto dist_at = [&](int ly, int b) -> int {
+      if (b <= 0 || !((S >> ly) & 1)) return b + 1;
+      return (int)((p0 >> ly) & 1) | ((int)((p1 >> ly) & 1) << 1) | ((int)((p2 >> ly) & 1) << 2) |
+             ((int)((p3 >> ly) & 1) << 3) | ((int)((p4 >> ly) & 1) << 4) | ((int)((p5 >> ly) & 1) << 5);
+    };
+    const size_t ea = (size_t)C.e * N + a;
+    bool fail = false;
+    if (crop) {
+      float* dst = s.dist_obs_out + ea * E * E + (size_t)(rr + ego) * E;
+      for (int c = 0; c < E; ++c) {
+        const int ly = ly0 - ego + c;
+        const int b = min(brow, min(ly, RB - 1 - ly) + 1);
+        const int d = dist_at(ly, b);
+        if (d > b) fail = true;
+        else dst[c] = dist_value((float)d, (float)M);
+      }
+    }
+    if (endr) {
+      auto end_cell = [&](int t, int ly) -> bool {
+        const int b = min(brow, min(ly, RB - 1 - ly) + 1);
+        const int d = dist_at(ly, b);
+        if (d > b) return !(fail = true);
+        pre[ea * 8 + 1 + t] = (float)d;
+        return true;
+      };
+      const bool ok0 = end_cell(er == 0 ? 0 : (er > 0 ? 1 : 3), ly0 - pad);
+      if (er == 0) {
+        end_cell(2, ly0 - pad + 1);
+        end_cell(4, ly0 - pad - 1);
+        if (ok0) pre[ea * 8] = (float)M;  // with target 0, as the loop above
+      }
+    }
+    if (fail) atomicOr((unsigned long long*)&L.sc->dist_fail, 1ull << a);
+  }
+}
+
 template <bool O32>
 __device__ __forceinline__ void st_tile(uint64_t* base, uint32_t idx, uint64_t v) {
   if constexpr (O32) *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(base) + (size_t)(idx << 3)) = v;
@@ -1391,7 +1513,7 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
 template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0, int RPLX = 0>
 __device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
                                                 Items<KI>& I) {
-  sense<NT, EPW, WT, SUK, KN, KM, RPLX>(s, C);
+  if (MC_ABL != 5) sense<NT, EPW, WT, SUK, KN, KM, RPLX>(s, C);
   __syncthreads();
   STAMP(13);
   if (s.sensor == 0) {
@@ -2044,7 +2166,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       // reward above, and in a multi-wave slot another wave may still be
       // there: every wave passes the reward before any POST store
       if constexpr (NT > 64 && !kPrePrefetch) __syncthreads();
-      dist_window<NT, EPW, WT>(s, C, skip);
+      if (MC_ABL != 1) {
+        if constexpr (MC_DIST_WIN != 0) dist_window_rows<NT, EPW, WT>(s, C, skip);
+        else dist_window<NT, EPW, WT>(s, C, skip);
+      }
       __syncthreads();
       dlist = C.sub < N && ((((skip | L.sc->dist_fail) >> C.sub) & 1ull) || L.dm[C.sub] < 0);
     }
@@ -2111,15 +2236,26 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   }
   if (s.dist) {
     // the full transform's work list (mc_dist.hip launch_dist_listed): one
-    // atomic per wave, the wave's entries at consecutive slots
+    // atomic per env slot of the wave on its env's shard (e % kListShards,
+    // spread over kListShards lines: early after a reset nearly every env
+    // appends, ~8k returning atomics per step on one address), the slot's
+    // entries at consecutive places of the shard
     const bool me = valid && dlist;
     const uint64_t m = __ballot(me);
     if (m) {
-      const int lane = (int)(threadIdx.x & 63), leader = __ffsll((unsigned long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(s.dist_cnt, (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, leader);
-      if (me) s.dist_cnt[5 + base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)e * (uint32_t)N + (uint32_t)C.sub;
+      const int lane = (int)(threadIdx.x & 63);
+      const uint64_t slotm = LPE >= 64 ? ~0ull : (low_mask(LPE) << (lane & ~(LPE - 1) & 63));
+      const uint64_t ms = m & slotm;
+      if (ms) {
+        const int leader = __ffsll((unsigned long long)ms) - 1;
+        const uint32_t sh = (uint32_t)e % (uint32_t)kListShards;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(s.dist_shc + sh * kShardStride, (uint32_t)__popcll(ms));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (me)
+          s.dist_cnt[5 + sh * s.dist_cap + base + __popcll(ms & ((1ull << lane) - 1ull))] =
+              (uint32_t)e * (uint32_t)N + (uint32_t)C.sub;
+      }
     }
     if (s.dist_full && blockIdx.x == 0 && threadIdx.x == 0) {  // the last step's full list is done
       s.dist_full[2] = s.dist_full[0];
@@ -2129,7 +2265,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   STAMP(8);
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && (NT == 64 || EPW == 1) &&
                 ObsFast<SH::EGO, SH::N, SH::LC>::NB <= 64) {
-    write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the workgroup
+    if (MC_ABL != 4) write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the workgroup
   } else {
     if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 16) ? SH::N : 0>(s, C, obs_out);
   }

@@ -122,6 +122,11 @@ struct State {
   // mc_dist.hip dist_kernel_t)
   float* dist_obs_out;
   uint32_t* dist_cnt;
+  // the work list's append counters, one per shard (env e appends to shard
+  // e % kListShards; counters kShardStride words apart), and the entries per
+  // shard: shard k's entries start at dist_cnt[5 + k * dist_cap]
+  uint32_t* dist_shc;
+  uint32_t dist_cap;
   // dist_reward: cumulative POST counters since mc_create (MC_FIELD_DIST_TOTALS):
   // maps listed, served by the top-cell cache, fully transformed, POST launches
   unsigned long long* dist_tot;
@@ -170,6 +175,8 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 #define MC_DIST_T 20
 #endif
 constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
+constexpr int kListShards = 8;        // dist work-list append counters (one address took every env's atomic)
+constexpr int kShardStride = 32;      // u32 words between them (a 128-B line each)
 constexpr int kDistStrips = 64;      // strips whose maxima the cache keeps (extended grids up to 2048 columns)
 constexpr int kDistT = MC_DIST_T;    // ... with d >= M0 - kDistT
 

@@ -45,7 +45,7 @@ def main():
     env.reset()
     for t in range(args.warmup):
         env.step(env.random_actions(7, t))
-    st = torch.zeros((B * 16 + 12288,), dtype=torch.int64, device=env.device)  # + per-part records
+    st = torch.zeros((B * 16 + 24576,), dtype=torch.int64, device=env.device)  # + per-part records
     _lib.check(env.lib.mc_debug_stamps(env._h, st.data_ptr()), "stamps")
     env.step(env.random_actions(7, args.warmup))
     torch.cuda.synchronize()
@@ -56,7 +56,11 @@ def main():
     s = s[s != 0]
     parts = allst[B * 16:B * 16 + 4096]
     parts = parts[parts != 0]
-    sub = allst[B * 16 + 8192:]
+    t0 = allst[B * 16 + 12288:B * 16 + 16384].astype(np.int64)
+    t1 = allst[B * 16 + 16384:B * 16 + 20480].astype(np.int64)
+    tk = allst[B * 16 + 20480:B * 16 + 24576].astype(np.int64)
+    live = t0 != 0
+    sub = allst[B * 16 + 8192:B * 16 + 12288]
     sub = sub[sub != 0]
     merged_tot = allst[B * 16 + 4096:B * 16 + 8192]
     merged_tot = (merged_tot[merged_tot != 0] & np.uint64(0xFFFFFF)).astype(np.int64) * 16
@@ -98,6 +102,13 @@ def main():
             g = [((sub >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.int64) * 16 for i in range(3)]
             print("    stage split: " + "  ".join(f"{lab} med {np.median(x):7.0f} p90 {np.percentile(x, 90):7.0f}"
                                               for lab, x in zip(("loads+transpose", "barrier", "extend rows"), g)))
+        if live.any():
+            base = tk[live].min()
+            print(f"    timeline (cycles from the first part's start): workgroup start med "
+                  f"{np.median(tk[live] - base):.0f} max {(tk[live] - base).max()}; item start med "
+                  f"{np.median(t0[live] - base):.0f} max {(t0[live] - base).max()}; part end med "
+                  f"{np.median(t1[live] - base):.0f} p90 {np.percentile(t1[live] - base, 90):.0f} max "
+                  f"{(t1[live] - base).max()}")
         if len(merged_tot):
             print(f"  merged parts (start -> done): n={len(merged_tot)} med {np.median(merged_tot):.0f} "
                   f"p90 {np.percentile(merged_tot, 90):.0f} max {merged_tot.max()}")
