@@ -803,12 +803,19 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           for (int k = 0; k < 2; ++k) {
             const int q = q0 + k * kDtThreads;
             const int ti = q / RWm, w = q - ti * RWm;
+            // tiles (ti, tj), (ti, tj + 1) of an even tj are adjacent in the
+            // block layout: one 16-byte load per pair (the block's padding
+            // columns exist; a tile past the last column reads as 0)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < 8; j += 2) {
               const int tj = 8 * w + j;
-              const uint64_t t = (q < nq && tj < s.TC) ? free_t[tile_index(s.TCS, ti, tj)] : 0ull;
-              lo[k][j] = (uint32_t)t;
-              hi[k][j] = (uint32_t)(t >> 32);
+              uint4 t = make_uint4(0u, 0u, 0u, 0u);
+              if (q < nq && tj < s.TC) t = *reinterpret_cast<const uint4*>(free_t + tile_index(s.TCS, ti, tj));
+              if (tj + 1 >= s.TC) t.z = t.w = 0u;
+              lo[k][j] = t.x;
+              hi[k][j] = t.y;
+              lo[k][j + 1] = t.z;
+              hi[k][j + 1] = t.w;
             }
           }
 #pragma unroll
