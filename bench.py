@@ -262,6 +262,12 @@ def main():
                          "launch per step); stream: K back-to-back Python/ctypes mc_step calls; graph: "
                          "uploaded hipGraph replay; events: per-launch HIP events")
     ap.add_argument("--eager", action="store_true", help="alias of --launch events")
+    ap.add_argument("--events", default="around", choices=["around", "after-first", "none"],
+                    help="native launch: where the HIP events that time the kernels sit in the timed region. "
+                         "around: before the first launch and after the last (kernel_us over K); after-first: "
+                         "after the first launch (a separate 1-launch mc_step_many call) and after the last "
+                         "(kernel_us over K - 1, no marker packet ahead of the first kernel); none: no events "
+                         "(kernel_us null)")
     ap.add_argument("--sync", default="default", choices=["default", "spin"],
                     help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is initialised, so "
                          "the host synchronize that closes the timed region spin-waits instead of sleeping")
@@ -354,7 +360,10 @@ def main():
     a0 = aptrs[0] if K else 0
     elapsed, kern_ms, issue_us = timed_launches(
         lambda i, st: env.step_raw(aptrs[i], rp, dp, op, st), dev, K, args.launch,
-        many_call=lambda st: native_call(env, a0, astride, K, rp, dp, op, st))
+        many_call=lambda st: native_call(env, a0, astride, K, rp, dp, op, st),
+        first_call=lambda st: (native_call(env, a0, astride, 1, rp, dp, op, st),
+                               native_call(env, a0 + astride, astride, K - 1, rp, dp, op, st)),
+        events=args.events)
     env.check()
     listed = dj_listed = served = dtot = None
     if dr:  # maps the last step sent to the full distance transform, and those the cache served (diagnostic)
@@ -373,6 +382,14 @@ def main():
 
     n_gpus = world
     value = aggregate_rate(total_envs, K, elapsed)
+    kern_from = KERNEL_US_FROM[args.launch]
+    if args.launch == "native" and args.events != "around":
+        if kern_ms is None:  # --events none: no events in the timed region
+            kern_ms = elapsed / K * 1e3
+            kern_from = "no events in the timed region (--events none): wall time per step"
+        else:
+            kern_from = ("HIP events after the first launch (its own mc_step_many call) and after the last: "
+                         "the K - 1 later launches / (K - 1) (includes kernel boundaries)")
     # §8(d): C5's float32 distance layer is 4 B per cell (100 B per agent at
     # E=5) and its two transforms read the whole bit map
     bpe = algorithmic_bytes_per_env_step(N, c["sensor_config"]["range"], cfg["egoradius"],
@@ -418,7 +435,7 @@ def main():
                 "global env id)",
         "config": {"workload": c["desc"], "envs_per_gpu": B, "global_envs": total_envs,
                    "launch": LAUNCH_DESC[args.launch], "host_issue_us_per_step": issue_us,
-                   "host_sync": args.sync,
+                   "host_sync": args.sync, "timing_events": args.events,
                    "kernel_variant": env.kernel_variant(),
                    **dist_desc(args, world),
                    "parallelism": f"env-shard x{n_gpus}", "auto_reset": True, "maxsteps": args.maxsteps,
@@ -431,7 +448,7 @@ def main():
                      "kernel": "mc::env_kernel" + (" + mc::dijkstra_window_kernel + mc::dijkstra_kernel (one step)"
                                                    if dj else " + the distance kernels (one step)" if dr else ""),
                      "kernel_us": round(kern_ms * 1e3, 3),
-                     "kernel_us_from": KERNEL_US_FROM[args.launch] + (" (every kernel of a step)" if dj or dr else ""),
+                     "kernel_us_from": kern_from + (" (every kernel of a step)" if dj or dr else ""),
                      "alg_bytes_per_env_step": bpe,
                      "achieved_from": "SURVEY 8(d) algorithmic bytes x envs / kernel_us",
                      "measured_traffic": measured,
@@ -484,7 +501,7 @@ def native_call(env, a0, astride, K, rp, dp, op, stream_ptr):
     return lambda: f(*args)
 
 
-def timed_launches(step_fn, dev, K, launch, many_call=None):
+def timed_launches(step_fn, dev, K, launch, many_call=None, first_call=None, events="around"):
     """Time K launches between barrier + synchronize; returns (elapsed s, ms
     per launch from HIP events on the launch stream, host issue time per
     step in us: from the first event record to the last launch returned).
@@ -509,7 +526,10 @@ def timed_launches(step_fn, dev, K, launch, many_call=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     stream = torch.cuda.current_stream(dev)
     if launch == "native":
-        return timed_native(many_call(stream.cuda_stream), dev, K, stream, world)
+        if events == "after-first" and K > 1:
+            c1, c2 = first_call(stream.cuda_stream)
+            return timed_native(c2, dev, K, stream, world, first=c1)
+        return timed_native(many_call(stream.cuda_stream), dev, K, stream, world, events=events != "none")
     graphs = []
     if launch == "graph":
         hip = ctypes.CDLL("libamdhip64.so")
@@ -565,9 +585,13 @@ def timed_launches(step_fn, dev, K, launch, many_call=None):
     return t1 - t0, ev0.elapsed_time(ev1) / K, issue_us
 
 
-def timed_native(call, dev, K, stream, world):
+def timed_native(call, dev, K, stream, world, first=None, events=True):
     """The native timed region: raw HIP events (ctypes) around one
-    mc_step_many call, between barrier + synchronize on both sides."""
+    mc_step_many call, between barrier + synchronize on both sides.  With
+    `first` (a 1-launch call issued before `call`, whose K - 1 launches the
+    events bracket) the first kernel has no marker packet ahead of it, and
+    the per-kernel time excludes its start from an idle queue; without
+    `events` the region holds the launches alone (per-kernel time None)."""
     import ctypes
 
     import torch
@@ -586,20 +610,28 @@ def timed_native(call, dev, K, stream, world):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    rec(ev[0], sp)
+    rc0 = 0
+    if first is not None:
+        rc0 = first()
+    if events:
+        rec(ev[0], sp)
     rc = call()
     t_issue = time.perf_counter()
-    rec(ev[1], sp)
+    if events:
+        rec(ev[1], sp)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    assert rc == 0, rc
+    assert rc0 == 0 and rc == 0, (rc0, rc)
     if world > 1:
         dist.barrier()
-    ms = ctypes.c_float(0.0)
-    assert hip.hipEventElapsedTime(ctypes.byref(ms), ev[0], ev[1]) == 0
+    per = None
+    if events:
+        ms = ctypes.c_float(0.0)
+        assert hip.hipEventElapsedTime(ctypes.byref(ms), ev[0], ev[1]) == 0
+        per = ms.value / (K - 1 if first is not None else K)
     for e in ev:
         hip.hipEventDestroy(e)
-    return t1 - t0, ms.value / K, round((t_issue - t0) / K * 1e6, 3)
+    return t1 - t0, per, round((t_issue - t0) / K * 1e6, 3)
 
 
 KERNEL_US_FROM = {
