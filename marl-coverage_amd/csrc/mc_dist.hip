@@ -88,7 +88,10 @@ constexpr int kMaxTrack = kDistStrips;         // strips whose max(d) the cache 
 #endif
 constexpr bool kOnePass = MC_DIST_ONEPASS != 0;
 #ifndef MC_FAST_TILES  // build knob (A/B): tiles the cache fast path stages (box + 25 around the robot)
-#define MC_FAST_TILES 2048
+// (1024 since round 5: 8 KB of LDS, more workgroups per CU; a box past it
+// sends the map to the full transform.  At the C5 steady state and early
+// phase the served counts were unchanged, profiles/r5/fast2/)
+#define MC_FAST_TILES 1024
 #endif
 constexpr int kFastTiles = MC_FAST_TILES;
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -1363,12 +1366,17 @@ size_t dist_static_lds_bytes() {
 // Build knobs (A/B, profiles/r4/c5_fast/): threads per workgroup and grid.
 // A wave per map (64 threads, 512 tiles, grid 4096) was slower: 52.9 vs
 // 28.1 us per step at the C5 steady state, the try's time scaling with the
-// threads it has
+// threads it has.  Round 5 (profiles/r5/fast/, fast2/): early after a reset
+// (~14,600 tries per step, ~7 per workgroup one after another) the tries
+// are bound by how many maps are in flight: 128 threads, 1,024 staged
+// tiles and a grid of 8,192 took the kernel from 57.5 to 40.5 us per step
+// (256 threads / 2,048 tiles / 2,048; 64 threads: 47.4), the steady state
+// 15.6 -> 16.7 us with the step unchanged (147.1 us both)
 #ifndef MC_FAST_THREADS
-#define MC_FAST_THREADS 256
+#define MC_FAST_THREADS 128
 #endif
 #ifndef MC_FAST_GRID
-#define MC_FAST_GRID 2048
+#define MC_FAST_GRID 8192
 #endif
 constexpr int kFastThreads = MC_FAST_THREADS;
 constexpr int kFastBuf = 128;  // full-list entries a workgroup buffers before one atomic
