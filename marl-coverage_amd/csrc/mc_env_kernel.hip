@@ -1869,6 +1869,11 @@ constexpr int env_min_waves() {
 #endif
   // C5 (16 agents): the robots in registers for the moves and the obs crops
   // would take the kernel past 128 VGPRs (3 waves per SIMD); keep 4
+// (round 5, profiles/r5/wpe/: 5 waves per SIMD spill 10 VGPRs, 82.1 ->
+// 87.3 us at the C5 steady state; 6 spill 28, 117.9 us)
+#ifdef MC_C5_WPE  // A/B knob: waves per SIMD the C5 shape must fit
+  if (SH::N == 16) return MC_C5_WPE;
+#endif
   return SH::N == 16 ? 4 : 1;
 }
 
