@@ -562,6 +562,26 @@ def test_batch_dist_multi_wave_slot(torch_cuda, name, monkeypatch):
     test_batch_matches_oracle(torch_cuda, name)
 
 
+def test_batch_dist_packed_slots(torch_cuda):
+    """dist_reward configs whose envs pack two to a wave (env_kernel<64,2,...>):
+    each env slot of the wave appends its listed maps to its own env's shard
+    of the full-transform work list (csrc/mc_env_kernel.hip, the slot-masked
+    ballot) -- the oracle comparison of every step covers the transform of
+    those entries (dec_grid_rl.py:222-223,239-240,260-282)."""
+    import marlcov
+    packed = []
+    for name in ("dist_lidar_n3", "dist_long_walk", "dist_wide_short", "dist_square_ego3"):
+        cfg, maker, B, _ = BATCH_CASES[name]
+        rs = np.random.RandomState(1)
+        env = marlcov.BatchCoverageEnv(cfg, B, grids=[maker(rs) for _ in range(B)], auto_reset=False)
+        if env.kernel_variant().startswith("env_kernel<64,2,"):
+            packed.append(name)
+        del env
+    assert packed, "no dist_reward batch case packs two envs per wave"
+    for name in packed:
+        test_batch_matches_oracle(torch_cuda, name)
+
+
 @pytest.mark.parametrize("full", [False, True], ids=["window", "full_map"])
 def test_dijkstra_far_targets(torch_cuda, monkeypatch, full):
     """dijkstra_input with the nearest unexplored cell 1..300 steps away
