@@ -1369,6 +1369,57 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
   }
 }
 
+// The same terms, agent-major, when the targets fit 32 lanes (T = 5 + E*E
+// <= 32, e.g. egoradius 2): lane l of the slot takes target l % 32 of agent
+// a0 + l / 32 in pass a0, so a lane's target offsets are computed once for
+// every pass (no per-item division into (agent, target) and (row, column)),
+// and an agent's skip / M test is uniform over its 32 lanes.
+template <int NT, int EPW, typename WT>
+__device__ __forceinline__ void dist_window_am(const State& s, const Ctx<NT, EPW, WT>& C, uint64_t skip) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int APP = LPE / 32;  // agents per pass
+  const Lds<WT>& L = C.L;
+  const int N = s.N, E = s.E, T = 5 + E * E, RB = 8 * s.TW;
+  const WT cols = sizeof(WT) == 8 && RB >= 64 ? ~(WT)0 : (WT)(((uint64_t)1 << RB) - 1);  // the block's columns
+  const int t = C.sub & 31;
+  if (t >= T) return;
+  // target - robot: the end cells of the next step at the quirk index, the crop
+  int ox, oy;
+  if (t < 5) {
+    ox = (t == 1 ? 1 : (t == 3 ? -1 : 0)) - s.pad;
+    oy = (t == 2 ? 1 : (t == 4 ? -1 : 0)) - s.pad;
+  } else {
+    const int k = t - 5, r = k / E;
+    ox = r - s.ego;
+    oy = k - r * E - s.ego;
+  }
+  float* pre_e = const_cast<float*>(s.dist_pre) + (size_t)C.e * N * 8;
+  float* obs_e = s.dist_obs_out + (size_t)C.e * N * E * E;
+  for (int a0 = 0; a0 < N; a0 += APP) {
+    const int a = a0 + (C.sub >> 5);
+    if (a >= N) break;
+    const int M = L.dm[a];
+    if (((skip >> a) & 1ull) || M < 0) continue;
+    const int lx = L.x[a] + ox - 8 * L.bx[a], ly = L.y[a] + oy - 8 * L.by[a];
+    const int b = min(min(lx, RB - 1 - lx), min(ly, RB - 1 - ly)) + 1;  // <= 0: outside the block
+    int d = b + 1;
+    if (b > 0) {
+      d = min(d, row_dist<WT>(L.fpr[row_word<WT>(s, a, lx)] & cols, ly));
+      for (int dr = 1; dr < d; ++dr) {
+        if (lx - dr >= 0) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx - dr)] & cols, ly));
+        if (lx + dr < RB) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx + dr)] & cols, ly));
+      }
+    }
+    if (d > b) {
+      atomicOr((unsigned long long*)&L.sc->dist_fail, 1ull << a);
+      continue;
+    }
+    if (t < 5) pre_e[a * 8 + 1 + t] = (float)d;
+    else obs_e[a * E * E + (t - 5)] = dist_value((float)d, (float)M);
+    if (t == 0) pre_e[a * 8] = (float)M;
+  }
+}
+
 // The same terms, one lane per (agent, target row): every target of the
 // agent lies in the rows px - ego .. px + ego (the crop) or px - pad - 1 ..
 // px - pad + 1 (the end cells at the quirk index), so N * 6 items at C5 where
@@ -1384,6 +1435,9 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
 // Tried, round 5 (profiles/r5/win/): C5 steady env kernel 83.6 us against
 // 81.7 with the loop above -- a lane's serial D steps, extractions and float
 // divisions cost more than the 4 balanced passes of (agent, target) items.
+#ifndef MC_DIST_AM  // build knob (A/B): 0 keeps the (agent, target) item loop for T <= 32
+#define MC_DIST_AM 1
+#endif
 #ifndef MC_DIST_WIN  // build knob (A/B): 1 runs dist_window_rows
 #define MC_DIST_WIN 0
 #endif
@@ -2172,8 +2226,14 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       // there: every wave passes the reward before any POST store
       if constexpr (NT > 64 && !kPrePrefetch) __syncthreads();
       if (MC_ABL != 1) {
-        if constexpr (MC_DIST_WIN != 0) dist_window_rows<NT, EPW, WT>(s, C, skip);
-        else dist_window<NT, EPW, WT>(s, C, skip);
+        if constexpr (MC_DIST_WIN != 0) {
+          dist_window_rows<NT, EPW, WT>(s, C, skip);
+        } else if constexpr (Ctx<NT, EPW, WT>::LPE % 32 == 0 && MC_DIST_AM) {
+          if (5 + s.E * s.E <= 32) dist_window_am<NT, EPW, WT>(s, C, skip);
+          else dist_window<NT, EPW, WT>(s, C, skip);
+        } else {
+          dist_window<NT, EPW, WT>(s, C, skip);
+        }
       }
       __syncthreads();
       dlist = C.sub < N && ((((skip | L.sc->dist_fail) >> C.sub) & 1ull) || L.dm[C.sub] < 0);
