@@ -547,6 +547,10 @@ constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
 #endif
 constexpr int kMaxParts = MC_MAX_PARTS;
 constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
+// the parts' candidate lists and counts are indexed by the map's full-list
+// index: S > 1 parts only when at most kSplitSlots / 2 maps are on the list
+// (State::dist_gcand was [B][N][kGCand], 2 GB at C5; now 4 MB)
+static_assert(kDistGSlots == kSplitSlots / 2, "State::dist_gcand's slots");
 #ifndef MC_DIST_FUSED  // build knob (A/B): 0 finalises split maps in a separate mode-3 launch
 #define MC_DIST_FUSED 1
 #endif
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (tid == 0) s_ccount = 0;
       __syncthreads();
       // the parts' candidates: a one-pass list (with theta0), else none
-      const uint32_t total = (kOnePass && theta0 > 0) ? ld_ho(s.dist_gcnt + ea, sc1) : 0u;
+      const uint32_t total = (kOnePass && theta0 > 0) ? ld_ho(s.dist_gcnt + fi, sc1) : 0u;
       const unsigned long long gk = ld_ho(s.dist_gkey + ea, sc1);
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
       for (int t = tid; t < T; t += kDtThreads)
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s_smax[st] = (int)ld_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, sc1);
       if (gk != 0 && total <= (uint32_t)kGCand)
         for (int k = tid; k < (int)total; k += kDtThreads) {
-          const int2 c = ld_ho(s.dist_gcand + (size_t)ea * kGCand + k, sc1);
+          const int2 c = ld_ho(s.dist_gcand + (size_t)fi * kGCand + k, sc1);
           if (c.y >= thr) {
             const int j = atomicAdd(&s_ccount, 1);
             if (j < kDistK) {
@@ -775,7 +779,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s_cov = gk != 0;  // a covered map's key is nonzero (its far or cell field)
         if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
         s.dist_gkey[ea] = 0;  // zero for the map's next split transform
-        s.dist_gcnt[ea] = 0;
+        s.dist_gcnt[fi] = 0;
       }
       __syncthreads();
     };
@@ -1164,13 +1168,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (kOnePass && theta0 > 0) {
         const int n = s_ccount;
         if (n > 0) {
-          if (tid == 0) s_base = atomicAdd(s.dist_gcnt + ea, (uint32_t)(n <= kDistK ? n : kGCand + 1));
+          if (tid == 0) s_base = atomicAdd(s.dist_gcnt + fi, (uint32_t)(n <= kDistK ? n : kGCand + 1));
           __syncthreads();
           const uint32_t base = s_base;
           if (n <= kDistK)
             for (int k = tid; k < n; k += kDtThreads)
               if (base + k < (uint32_t)kGCand)
-                st_ho(s.dist_gcand + (size_t)ea * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused);
+                st_ho(s.dist_gcand + (size_t)fi * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused);
         }
       }
       if constexpr (kFused) {

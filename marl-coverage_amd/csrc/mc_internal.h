@@ -151,8 +151,9 @@ struct State {
   // stores, mc_dist.hip)
   uint32_t* dist_sm;
   // with the cache: the split full transform's per-map partials (mc_dist.hip
-  // modes 2 / 3; zero between uses): the best key, the candidate cells
-  // published and the candidates [B][N][4 * kDistK] (cell, d)
+  // modes 2 / 3; zero between uses): the best key [B][N]; by full-list index
+  // (< kDistGSlots) the candidate cells published and the candidates
+  // [kDistGSlots][4 * kDistK] (cell, d)
   unsigned long long* dist_gkey;
   uint32_t* dist_gcnt;
   int2* dist_gcand;
@@ -175,6 +176,7 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 #define MC_DIST_T 20
 #endif
 constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
+constexpr int kDistGSlots = 256;      // full-list entries a split transform can split (mc_dist.hip kSplitSlots / 2)
 constexpr int kListShards = 8;        // dist work-list append counters (one address took every env's atomic)
 constexpr int kShardStride = 32;      // u32 words between them (a 128-B line each)
 constexpr int kDistStrips = 64;      // strips whose maxima the cache keeps (extended grids up to 2048 columns)
