@@ -51,7 +51,23 @@ __device__ __forceinline__ int32_t pack_witness(int x, int y) {
 __device__ __forceinline__ bool bits_within(uint64_t nb, int x0, int y0, int wx, int wy, int M) {
   const int bx = max(0, max(x0 - wx, wx - (x0 + 7)));
   const int by = max(0, max(y0 - wy, wy - (y0 + 7)));
-  if (bx + by >= M) return false;
+  if (bx + by >= M || !nb) return false;
+  // the set bits' bounding box (rows: a bit per nonzero byte; columns: the
+  // OR of the bytes): no bit within M if the box is not, every bit within M
+  // if its far corner is -- the row walk below only for the boxes between
+  uint64_t t = nb | (nb >> 4);
+  t |= t >> 2;
+  t |= t >> 1;
+  const uint32_t rows = (uint32_t)(((t & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+  uint64_t c = nb | (nb >> 32);
+  c |= c >> 16;
+  c |= c >> 8;
+  const uint32_t cols = (uint32_t)c & 0xFFu;
+  const int r0 = x0 + __ffs(rows) - 1, r1 = x0 + 31 - __clz(rows);
+  const int c0 = y0 + __ffs(cols) - 1, c1 = y0 + 31 - __clz(cols);
+  const int lb = max(0, max(r0 - wx, wx - r1)) + max(0, max(c0 - wy, wy - c1));
+  if (lb >= M) return false;
+  if (max(abs(wx - r0), abs(wx - r1)) + max(abs(wy - c0), abs(wy - c1)) < M) return true;
   const int p = wy - y0;  // witness column relative to the tile
   for (int r = 0; r < 8; ++r) {
     const uint32_t row = (uint32_t)(nb >> (8 * r)) & 0xFFu;
