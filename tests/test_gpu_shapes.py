@@ -319,6 +319,34 @@ def test_c5_top_cell_cache_is_exact(torch_cuda, monkeypatch):
         assert torch.equal(a[4][known], b[4][known]), f"step {t}: max_d"
 
 
+def test_c5_unsplit_transform_is_identical(torch_cuda, monkeypatch):
+    """MARLCOV_DIST_SPLIT=0 (each listed map tried and, if needed, transformed
+    whole by one workgroup: dist_kernel_t mode 1, reading the env kernel's
+    sharded work list directly) against the default path (cache tries in
+    dist_fast_kernel, full transforms split over parts): 64 C5 envs x 80
+    steps of the same device actions give bit-identical obs, distance layers,
+    rewards and dones (dec_grid_rl.py:222-223,239-240,260-282)."""
+    import marlcov
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=50)
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("MARLCOV_DIST_SPLIT", split)
+        env = marlcov.BatchCoverageEnv(cfg, 64, gen=dict(width=512, length=512, prob_obst=0.1, seed=1001),
+                                       seed=9, auto_reset=True)
+        assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+        env.reset()
+        acc = []
+        for t in range(80):
+            obs, rew, done = env.step(env.random_actions(31, t))
+            acc.append((obs.clone(), env.dist_obs.clone(), rew.clone(), done.clone()))
+        outs.append(acc)
+        del env
+    for t, (a, b) in enumerate(zip(*outs)):
+        for x, y, name in zip(a, b, ("obs", "dist_obs", "reward", "done")):
+            assert torch.equal(x, y), f"step {t}: {name}"
+
+
 def test_c5_cache_steady_state_matches_oracle(torch_cuda, monkeypatch):
     """The top-cell cache where the C5 bench line gets its speed: 256 C5 envs
     (16 agents, 512 x 512, dist_reward, 2000-step episodes) run 600 device
