@@ -1369,6 +1369,9 @@ __device__ __forceinline__ void dist_window(const State& s, const Ctx<NT, EPW, W
   }
 }
 
+#ifndef MC_DIST_AM  // build knob (A/B): 0 keeps the (agent, target) item loop for T <= 32
+#define MC_DIST_AM 1
+#endif
 // The same terms, agent-major, when the targets fit 32 lanes (T = 5 + E*E
 // <= 32, e.g. egoradius 2): lane l of the slot takes target l % 32 of agent
 // a0 + l / 32 in pass a0, so a lane's target offsets are computed once for
@@ -1417,121 +1420,6 @@ __device__ __forceinline__ void dist_window_am(const State& s, const Ctx<NT, EPW
     if (t < 5) pre_e[a * 8 + 1 + t] = (float)d;
     else obs_e[a * E * E + (t - 5)] = dist_value((float)d, (float)M);
     if (t == 0) pre_e[a * 8] = (float)M;
-  }
-}
-
-// The same terms, one lane per (agent, target row): every target of the
-// agent lies in the rows px - ego .. px + ego (the crop) or px - pad - 1 ..
-// px - pad + 1 (the end cells at the quirk index), so N * 6 items at C5 where
-// the loop above ran N * (5 + E * E).  A lane grows the set of its row's
-// cells within L1 distance D of a covered block cell, D = 0, 1, ..:
-//   S_D = S_{D-1} | S_{D-1} << 1 | S_{D-1} >> 1 | row(lx - D) | row(lx + D)
-// (cells of row lx within D of a covered cell of rows lx - D' .. lx + D'), and
-// a cell's d is the first D whose S_D holds it, recorded in five bit planes.
-// It stops once every target of the row is reached or D passes the largest
-// bound b of its targets (d > b: the agent goes to the full transform, as
-// above).  Rows outside the block read as empty, columns are the block's:
-// the same block-restricted distance as the row scans above.
-// Tried, round 5 (profiles/r5/win/): C5 steady env kernel 83.6 us against
-// 81.7 with the loop above -- a lane's serial D steps, extractions and float
-// divisions cost more than the 4 balanced passes of (agent, target) items.
-#ifndef MC_DIST_AM  // build knob (A/B): 0 keeps the (agent, target) item loop for T <= 32
-#define MC_DIST_AM 1
-#endif
-#ifndef MC_DIST_WIN  // build knob (A/B): 1 runs dist_window_rows
-#define MC_DIST_WIN 0
-#endif
-template <int NT, int EPW, typename WT>
-__device__ __forceinline__ void dist_window_rows(const State& s, const Ctx<NT, EPW, WT>& C, uint64_t skip) {
-  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
-  const Lds<WT>& L = C.L;
-  const int N = s.N, E = s.E, ego = s.ego, pad = s.pad, RB = 8 * s.TW;
-  const WT cols = sizeof(WT) == 8 && RB >= 64 ? ~(WT)0 : (WT)(((uint64_t)1 << RB) - 1);  // the block's columns
-  const int r_lo = min(-ego, -pad - 1), r_hi = max(ego, -pad + 1), NR = r_hi - r_lo + 1;
-  float* pre = const_cast<float*>(s.dist_pre);
-  for (int idx = C.sub; idx < N * NR; idx += LPE) {
-    const int a = idx / NR, rr = r_lo + (idx - a * NR);
-    const int M = L.dm[a];
-    if (((skip >> a) & 1ull) || M < 0) continue;
-    const int px = L.x[a], py = L.y[a];
-    const int lx = px + rr - 8 * L.bx[a];  // this lane's block row
-    const int ly0 = py - 8 * L.by[a];      // the robot's block column
-    const bool crop = rr >= -ego && rr <= ego;
-    const int er = rr + pad;               // end cells: rows -pad - 1 .. -pad + 1 (t 3, 0 / 2 / 4, 1)
-    const bool endr = er >= -1 && er <= 1;
-    // the row's targets: the crop's E cells (columns ly0 - ego ..), the end
-    // cells (column ly0 - pad, and ly0 - pad +- 1 in row -pad); bound
-    // b = distance to the block's edge + 1 (<= 0: outside the block)
-    const int brow = min(lx, RB - 1 - lx) + 1;
-    int bmax = -1;
-    WT tmask = 0;
-    auto add_target = [&](int ly) {
-      const int b = min(brow, min(ly, RB - 1 - ly) + 1);
-      bmax = max(bmax, b);
-      if (b > 0) tmask |= (WT)1 << ly;
-    };
-    if (crop)
-      for (int c = 0; c < E; ++c) add_target(ly0 - ego + c);
-    if (endr) {
-      add_target(ly0 - pad);
-      if (er == 0) {
-        add_target(ly0 - pad + 1);
-        add_target(ly0 - pad - 1);
-      }
-    }
-    // grow S while some target is unreached and D <= bmax
-    WT S = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;  // (b <= 32: D < 64)
-    if (bmax > 0) {
-      S = L.fpr[row_word<WT>(s, a, lx)] & cols;
-      for (int D = 1; D <= bmax && (S & tmask) != tmask; ++D) {
-        WT n = S | (S << 1) | (S >> 1);
-        if (lx - D >= 0) n |= L.fpr[row_word<WT>(s, a, lx - D)];
-        if (lx + D < RB) n |= L.fpr[row_word<WT>(s, a, lx + D)];
-        n &= cols;
-        const WT nb = n & ~S;
-        p0 |= (D & 1) ? nb : (WT)0;
-        p1 |= (D & 2) ? nb : (WT)0;
-        p2 |= (D & 4) ? nb : (WT)0;
-        p3 |= (D & 8) ? nb : (WT)0;
-        p4 |= (D & 16) ? nb : (WT)0;
-        p5 |= (D & 32) ? nb : (WT)0;
-        S = n;
-      }
-    }
-    // d of block column ly (b + 1 when unreached)
-    auto dist_at = [&](int ly, int b) -> int {
-      if (b <= 0 || !((S >> ly) & 1)) return b + 1;
-      return (int)((p0 >> ly) & 1) | ((int)((p1 >> ly) & 1) << 1) | ((int)((p2 >> ly) & 1) << 2) |
-             ((int)((p3 >> ly) & 1) << 3) | ((int)((p4 >> ly) & 1) << 4) | ((int)((p5 >> ly) & 1) << 5);
-    };
-    const size_t ea = (size_t)C.e * N + a;
-    bool fail = false;
-    if (crop) {
-      float* dst = s.dist_obs_out + ea * E * E + (size_t)(rr + ego) * E;
-      for (int c = 0; c < E; ++c) {
-        const int ly = ly0 - ego + c;
-        const int b = min(brow, min(ly, RB - 1 - ly) + 1);
-        const int d = dist_at(ly, b);
-        if (d > b) fail = true;
-        else dst[c] = dist_value((float)d, (float)M);
-      }
-    }
-    if (endr) {
-      auto end_cell = [&](int t, int ly) -> bool {
-        const int b = min(brow, min(ly, RB - 1 - ly) + 1);
-        const int d = dist_at(ly, b);
-        if (d > b) return !(fail = true);
-        pre[ea * 8 + 1 + t] = (float)d;
-        return true;
-      };
-      const bool ok0 = end_cell(er == 0 ? 0 : (er > 0 ? 1 : 3), ly0 - pad);
-      if (er == 0) {
-        end_cell(2, ly0 - pad + 1);
-        end_cell(4, ly0 - pad - 1);
-        if (ok0) pre[ea * 8] = (float)M;  // with target 0, as the loop above
-      }
-    }
-    if (fail) atomicOr((unsigned long long*)&L.sc->dist_fail, 1ull << a);
   }
 }
 
@@ -2226,9 +2114,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       // there: every wave passes the reward before any POST store
       if constexpr (NT > 64 && !kPrePrefetch) __syncthreads();
       if (MC_ABL != 1) {
-        if constexpr (MC_DIST_WIN != 0) {
-          dist_window_rows<NT, EPW, WT>(s, C, skip);
-        } else if constexpr (Ctx<NT, EPW, WT>::LPE % 32 == 0 && MC_DIST_AM) {
+        // (tried, round 5: one lane per (agent, target row) growing the
+        // row's covered set by a bit-parallel dilation -- 83.6 against 81.7
+        // us at the C5 steady state, profiles/r5/win/; removed)
+        if constexpr (Ctx<NT, EPW, WT>::LPE % 32 == 0 && MC_DIST_AM) {
           if (5 + s.E * s.E <= 32) dist_window_am<NT, EPW, WT>(s, C, skip);
           else dist_window<NT, EPW, WT>(s, C, skip);
         } else {
