@@ -5,10 +5,13 @@
 One "step" = one launch of the HIP env kernel advancing every env of this
 GPU's shard by one timestep (all agents move, sense, merge, reward, done,
 obs, auto-reset).  Inputs (grids, state, per-step action bytes) are resident
-in HBM before the timed region.  N>1: one process per GPU (torchrun), each
-rank owns an independent env shard (weak scaling, no collective on the step
-path); RCCL is used once after timing for the scalar episode-return
-all-reduce and the max-over-ranks time.
+in HBM before the timed region.  N>1: one process per GPU, each rank owns an
+independent env shard (weak scaling, no collective on the step path); RCCL
+is used once after timing for the scalar episode-return all-reduce and the
+max-over-ranks time.  Under torchrun the ranks come from its env; a plain
+`python bench.py --gpus N` starts `torch.distributed.run --nproc-per-node N`
+itself as a child (launch_ranks) and exits with its code.  A world size that
+differs from --gpus, or more RCCL ranks than visible GPUs, exits non-zero.
 """
 from __future__ import annotations
 
@@ -88,8 +91,11 @@ def algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3, full_map
 
 DJ_WINDOW_CELLS = 64 * 64  # csrc/mc_dijkstra.hip: dijkstra_window_kernel
 
-DIST_CACHE_CELLS = 512      # csrc/mc_dist.hip kDistK: top-cell cache entries per map
-DIST_CACHE_BYTES = DIST_CACHE_CELLS * 8 + 32  # i32 cell + i32 d per entry, 32-B header
+def dist_cache_bytes():
+    """Bytes of one map's top-cell cache: kDistK (the library's build
+    constant, mc_build_param) x (i32 cell + i32 d) + the 32-B header."""
+    from marlcov import _lib
+    return _lib.load().mc_build_param(_lib.PARAM_DIST_CACHE_CELLS) * 8 + 32
 
 
 def c5_design_bytes_per_step(B, n_agents, beam_range, ego, ext_side, listed, served, full, launches):
@@ -107,7 +113,8 @@ def c5_design_bytes_per_step(B, n_agents, beam_range, ego, ext_side, listed, ser
     timed."""
     window = algorithmic_bytes_per_env_step(n_agents, beam_range, ego, layers=3 + 4)
     per_map = math.ceil(ext_side * ext_side / 8)
-    extra = full * (per_map + DIST_CACHE_BYTES) + served * DIST_CACHE_BYTES + listed * 4
+    cb = dist_cache_bytes()
+    extra = full * (per_map + cb) + served * cb + listed * 4
     return B * window + (extra / launches if launches else 0.0)
 
 
@@ -116,8 +123,13 @@ def c5_design_bytes_per_step(B, n_agents, beam_range, ego, ext_side, listed, ser
 # per-cell Python beam march and full-map copies) in P independent processes.
 # Runs BEFORE the GPU is touched (fork-safe).
 # ---------------------------------------------------------------------------
+# at least 2 s per process, and at C4 / C5 at least 20 steps
+CPU_MIN_STEPS = {"c4": 20, "c5": 20}
+
+
 def _cpu_worker(args):
     seed, secs, cfgname = args
+    min_steps = CPU_MIN_STEPS.get(cfgname, 8)
     import numpy as np
     from oracle.cpu_ref import DecGridRLRef
 
@@ -138,7 +150,7 @@ def _cpu_worker(args):
         n += 1
         if done:
             env.reset(False, None)
-        if n % 8 == 0 and time.perf_counter() - t0 >= secs:
+        if n >= min_steps and n % 8 == 0 and time.perf_counter() - t0 >= secs:
             break
     return n, time.perf_counter() - t0
 
@@ -275,13 +287,30 @@ def main():
                     help="process group for N > 1 (nccl = RCCL over xGMI).  gloo rehearses the "
                          "multi-rank flow on fewer GPUs than ranks (ranks share the visible GPUs "
                          "round-robin; the rate is then not a scaling number)")
+    ap.add_argument("--plan", action="store_true",
+                    help="print the ranks' shard plan (world, env ranges, seeds) as rank 0's JSON line and exit "
+                         "without touching a GPU (checks the launcher and the sharding on CPU)")
     args = ap.parse_args()
     if args.eager:
         args.launch = "events"
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `python bench.py --gpus N`: start the N ranks ourselves (before
+        # any GPU call) and relay their exit code; rank 0 prints the line
+        return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to print a line for a "
+              "different GPU count", file=sys.stderr)
+        return 2
+    if args.dist_backend == "nccl" and not args.plan:
+        visible = visible_gpus()
+        if args.gpus > visible:
+            print(f"bench.py: --gpus {args.gpus} with RCCL needs {args.gpus} GPUs, {visible} visible",
+                  file=sys.stderr)
+            return 2
     c = CONFIGS[args.config]
     # this rank's slice [e0, e1) of the global env batch; every device random
     # stream is keyed by the global env id (marlcov.shards), so env e runs the
@@ -297,6 +326,8 @@ def main():
     total_envs = args.global_envs or B * world
     if args.maxsteps is None:
         args.maxsteps = c.get("maxsteps", 1000)
+    if args.plan:
+        return print_plan(args, world, rank, e0, e1, total_envs, scaling)
 
     cpu = None
     if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu:
@@ -459,6 +490,55 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def visible_gpus():
+    """HIP devices this process may use (torch.cuda.device_count() does not
+    initialise the GPU on this image, so the launcher can call it)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` without torchrun: run N ranks as a CHILD
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same args>`
+    (this process never touches the GPU, so no exec after GPU init), relay
+    the child's exit code.  Rank 0 prints the JSON line to the inherited
+    stdout.  With RCCL, N above the visible GPU count is an error here, not a
+    line for fewer GPUs."""
+    import socket
+    import subprocess
+    if args.dist_backend == "nccl" and not args.plan:
+        visible = visible_gpus()
+        if args.gpus > visible:
+            print(f"bench.py: --gpus {args.gpus} with RCCL needs {args.gpus} GPUs, {visible} visible",
+                  file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    sys.stdout.flush()
+    return subprocess.call(cmd)
+
+
+def print_plan(args, world, rank, e0, e1, total_envs, scaling):
+    """--plan: every rank's shard (env range and the seeds keyed by its global
+    env offset) gathered to rank 0, printed as one JSON line; no GPU work."""
+    from marlcov.shards import shard_seeds
+    mine = {"rank": rank, "env_range": [e0, e1], "seeds": shard_seeds(e0)}
+    plans = [mine]
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        plans = [None] * world
+        dist.all_gather_object(plans, mine)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"plan": plans, "n_gpus": world, "global_envs": total_envs, "scaling": scaling,
+                          "config": args.config, "dist_backend": args.dist_backend}), flush=True)
+    return 0
 
 
 def set_spin_sync(local):
@@ -721,4 +801,4 @@ def bench_super(args, c, B, cpu, world, rank, dev, run):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MARLCOV_ABI_VERSION 8
+#define MARLCOV_ABI_VERSION 9
 
 enum {
   MC_OK = 0,
@@ -163,6 +163,14 @@ const char* mc_last_error(void);
  * (2) / sizeof(mc_sg_layout) (3): lets an FFI binding verify its struct
  * mirrors. */
 int64_t mc_struct_size(int32_t which);
+
+/* Build-time constants a caller prices or sizes work with (ABI v9): the
+ * top-cell cache's cells per map (kDistK, MC_DIST_K build knob), its
+ * threshold (kDistT: the cache holds every cell with d >= M0 - kDistT) and
+ * the largest extended grid (rows) the distance transform takes.  -1 for an
+ * unknown `which`. */
+enum { MC_PARAM_DIST_CACHE_CELLS = 0, MC_PARAM_DIST_T = 1, MC_PARAM_DIST_MAX_ROWS = 2 };
+int64_t mc_build_param(int32_t which);
 
 /* Allocate device state for cfg->num_envs envs on HIP device `hip_device`.
  * Replaces DecGridRL.__init__ (dec_grid_rl.py:30-89) minus the first reset. */

@@ -11,10 +11,11 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmarlcov.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 MC_OK, MC_EINVAL, MC_EHIP, MC_ESTATE, MC_EDEVICE = 0, -1, -2, -3, -4
 SENSOR_LIDAR, SENSOR_SQUARE = 0, 1
+PARAM_DIST_CACHE_CELLS, PARAM_DIST_T, PARAM_DIST_MAX_ROWS = 0, 1, 2  # mc_build_param
 ACT_SENTINEL = 255
 ACT_NOOP = 4
 
@@ -124,6 +125,7 @@ SIGNATURES = [
     ("mc_abi_version", _I32, []),
     ("mc_last_error", ctypes.c_char_p, []),
     ("mc_struct_size", _I64, [_I32]),
+    ("mc_build_param", _I64, [_I32]),
     ("mc_create", ctypes.c_int, [ctypes.POINTER(McConfig), ctypes.c_int, ctypes.POINTER(_VP)]),
     ("mc_destroy", None, [_VP]),
     ("mc_query", ctypes.c_int, [_VP, ctypes.POINTER(McLayout)]),

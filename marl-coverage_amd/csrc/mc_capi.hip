@@ -192,6 +192,15 @@ int64_t mc_struct_size(int32_t which) {
   }
 }
 
+int64_t mc_build_param(int32_t which) {
+  switch (which) {
+    case MC_PARAM_DIST_CACHE_CELLS: return mc::kDistK;
+    case MC_PARAM_DIST_T: return mc::kDistT;
+    case MC_PARAM_DIST_MAX_ROWS: return mc::dist_max_rows();
+    default: return -1;
+  }
+}
+
 int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
   if (!cfg || !out_env) return fail(MC_EINVAL, "mc_create: null argument");
   *out_env = nullptr;

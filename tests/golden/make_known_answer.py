@@ -1,10 +1,13 @@
-"""Capture the reference's published known answer (SURVEY §8(c) pin 3).
+"""Capture the reference's known answer (SURVEY §8(c) pin 3).
 
 The reference's only published result: the non-learning controllers BSA and
 BA* cover 100 % of the hand-made test grids (``gridload(None)``,
-``Utils/gridmaker.py:23-43``) in every test episode, with total reward 234
-(``Example_Experiments/Non_Learning/BSA/Example/TerminalOutput.txt:3325-3326``,
-``.../BA_Star/Example/TerminalOutput.txt:172-173``).
+``Utils/gridmaker.py:23-43``) in every test episode
+(``Example_Experiments/Non_Learning/BA_Star/Example/TerminalOutput.txt:172-173``
+says "100.0 percent"; the BSA log records the same runs).  The total reward
+of each episode, 234 (205 free cells - 1 + 30 terminal), is NOT published:
+it was captured by running the reference's own DecGridRL / BSA / BA* here,
+in the build container, and is pinned by this fixture alone.
 
 Runs ONLY in the build container, where the read-only reference checkout is
 mounted at /root/reference.  It imports the reference's ``DecGridRL``,

@@ -15,7 +15,7 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def case_names():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith(("beam_tables", "known_answer")))
+                  if not os.path.basename(p).startswith(("beam_tables", "known_answer", "bg2_")))
 
 
 def load_case(name):
@@ -117,25 +117,30 @@ def check_against_golden(env):
 KNOWN_ANSWER_POLICIES = ("bsa", "ba_star")
 
 
-def load_known_answer():
-    z = np.load(os.path.join(GOLDEN_DIR, "known_answer.npz"), allow_pickle=False)
+def load_known_answer(name="known_answer.npz"):
+    z = np.load(os.path.join(GOLDEN_DIR, name), allow_pickle=False)
     return {k: z[k] for k in z.files}
 
 
-def replay_known_answer(env_cls, ka, policy):
+def replay_known_answer(env_cls, ka, policy, expect=(234.0, 1.0)):
     """Replay every recorded test episode of ``policy`` through ``env_cls``
     (the oracle or the HIP facade) the way ``test_RLalg`` runs it
     (Utils/utils.py:6-44,111-149): one env over the hand-made test grids,
     ``np.random.seed(seed)`` then ``reset(True, ind)``, then the controller's
     recorded actions.  Observation, reward and done must equal the record at
-    every step; each episode must end done with percent_covered() == 1.0 and
-    total reward 234.  Returns the per-episode (total reward, percent covered)."""
+    every step; each episode must end done with the recorded total reward and
+    percent_covered(), which must be ``expect`` when given (BSA / BA*: 234
+    and 1.0).  A record with ``<policy>__max_steps`` was cut there (the
+    capture lowered ``_test_maxsteps``, generate_episode's cut).  Returns the
+    per-episode (total reward, percent covered)."""
     pre = policy + "__"
     config = json.loads(ka[pre + "env_config"].tobytes().decode())
     test = [g.astype(np.float64) for g in ka["test_grids"]]
     train = [g.astype(np.float64) for g in ka["train_grids"]]
     with contextlib.redirect_stdout(io.StringIO()):
         env = env_cls(train, config, use_graph=False, test_set=test)
+    if pre + "max_steps" in ka:
+        env._test_maxsteps = int(ka[pre + "max_steps"])
     n_ep = len(ka[pre + "ep_len"])
     off = np.concatenate([[0], np.cumsum(ka[pre + "ep_len"])])
     results = []
@@ -163,7 +168,9 @@ def replay_known_answer(env_cls, ka, policy):
             total += r
         pc = env.percent_covered()
         assert done, tag
-        assert total == ka[pre + "ep_total"][e] == 234.0, (tag, total)
-        assert pc == ka[pre + "ep_pc"][e] == 1.0, (tag, pc)
+        assert total == ka[pre + "ep_total"][e], (tag, total)
+        assert pc == ka[pre + "ep_pc"][e], (tag, pc)
+        if expect is not None:
+            assert (total, pc) == expect, (tag, total, pc)
         results.append((total, pc))
     return results

@@ -82,8 +82,9 @@ def device_invariants(torch, env, tag):
     assert not bool((key[:, 1:] == key[:, :-1]).any()), f"{tag}: two robots on one cell"
 
 
-def bench_env(cfgname, maxsteps):
-    """The env exactly as bench.py main() builds it for this config."""
+def bench_env(cfgname, maxsteps, rank=0):
+    """The env exactly as bench.py main() builds it for this config on rank
+    ``rank`` (weak scaling: the shard of global envs [rank*B, (rank+1)*B))."""
     import bench
     import marlcov
     from marlcov.shards import shard_seeds
@@ -91,17 +92,21 @@ def bench_env(cfgname, maxsteps):
     cfg = dict(bench.BASE, numrobot=c["numrobot"], sensor_config=c["sensor_config"], allow_even_beams=True,
                maxsteps=maxsteps, **c.get("extra", {}))
     B = c["envs"]
-    seeds = shard_seeds(0)
+    seeds = shard_seeds(rank * B)
     env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=c["width"], length=c["width"], prob_obst=0.1,
                                                     seed=seeds["grid_seed"], num_grids=B),
                                    seed=seeds["env_seed"], auto_reset=True, env_offset=seeds["env_offset"])
     return env, cfg, seeds
 
 
-def run_full_size(torch, cfgname, maxsteps, steps, sample, variant, inv_every, dist_every=0):
-    """Bench-shaped env; the sample tracked by the oracle from the reset."""
+def run_full_size(torch, cfgname, maxsteps, steps, sample, variant, inv_every, dist_every=0, rank=0):
+    """Bench-shaped env of rank ``rank``'s shard; the sample tracked by the
+    oracle from the reset.  The sampled envs' pool grids and start cells are
+    checked against the host restatement of the streams at their GLOBAL ids
+    (offset + b), so a late rank's shard is the global batch's slice."""
     from marlcov import _lib, streams
-    env, cfg, seeds = bench_env(cfgname, maxsteps)
+    env, cfg, seeds = bench_env(cfgname, maxsteps, rank)
+    off = seeds["env_offset"]
     assert env.kernel_variant() == variant, env.kernel_variant()
     B, N = env.num_envs, env.num_agents
     env.reset()
@@ -110,8 +115,12 @@ def run_full_size(torch, cfgname, maxsteps, steps, sample, variant, inv_every, d
     for b in sample:
         g = int(st["env_grid"][b])
         grid = np.where(st["neg"][g] == 1, -1.0, np.where(st["pos_plane"][g] == 1, 1.0, 0.0))
-        np.testing.assert_array_equal(st["pos"][b], streams.start_cells(seeds["env_seed"], b, int(st["episode"][b]),
-                                                                        grid, N), err_msg=f"reset cells {b}")
+        np.testing.assert_array_equal(grid, streams.generated_grid(seeds["grid_seed"], 0.1, grid.shape[0],
+                                                                   grid.shape[1], off + g),
+                                      err_msg=f"pool grid {g} at global id {off + g}")
+        np.testing.assert_array_equal(st["pos"][b], streams.start_cells(seeds["env_seed"], off + b,
+                                                                        int(st["episode"][b]), grid, N),
+                                      err_msg=f"reset cells {b}")
         np.random.seed(0)
         from oracle.cpu_ref import DecGridRLRef
         ref = DecGridRLRef([grid[1:-1, 1:-1]], cfg)
@@ -137,7 +146,7 @@ def run_full_size(torch, cfgname, maxsteps, steps, sample, variant, inv_every, d
             if d:
                 resets += 1
                 p = st["pos"][b]
-                want = streams.start_cells(seeds["env_seed"], b, int(st["episode"][b]), refs[b]._grid, N)
+                want = streams.start_cells(seeds["env_seed"], off + b, int(st["episode"][b]), refs[b]._grid, N)
                 np.testing.assert_array_equal(p, want, err_msg=tag + " start cells vs host Philox")
                 o, _ = refs[b].reset(False, None, positions=[tuple(q) for q in p])
             np.testing.assert_array_equal(obs_h[b], o, err_msg=tag + " obs")
@@ -150,12 +159,15 @@ def run_full_size(torch, cfgname, maxsteps, steps, sample, variant, inv_every, d
     return env, resets, listed, cached
 
 
-def test_c2_bench_shape_full_size(torch_cuda):
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c2_bench_shape_full_size(torch_cuda, rank):
     """C2 (configs[1], the metric's workload): 4,096 envs, 4 agents, 128x128,
     21 beams R=10; maxsteps 20 so every env auto-resets three times in 64
-    steps; 16 envs tracked by the oracle from the reset."""
+    steps; 16 envs tracked by the oracle from the reset.  rank 7: the last
+    shard of C3 (global envs 28,672..32,767 of 8 x 4,096)."""
     sample = [int(b) for b in np.random.RandomState(2).choice(4096, 16, replace=False)]
-    env, resets, _, _ = run_full_size(torch_cuda, "c2", 20, 64, sample, "env_kernel<64,2,u32,C2>", inv_every=8)
+    env, resets, _, _ = run_full_size(torch_cuda, "c2", 20, 64, sample, "env_kernel<64,2,u32,C2>", inv_every=8,
+                                      rank=rank)
     assert resets >= 3 * len(sample)
     ep = env.get_state(__import__("marlcov")._lib.FIELD_EPISODE)
     assert int(ep.min()) >= 4  # every env of the batch: the first episode + 3 auto-resets
@@ -173,7 +185,8 @@ def test_c4_bench_shape_full_size(torch_cuda):
     assert int(env.get_state(__import__("marlcov")._lib.FIELD_EPISODE).min()) >= 4
 
 
-def test_c5_bench_shape_full_size(torch_cuda):
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c5_bench_shape_full_size(torch_cuda, rank):
     """C5 (configs[4], one GPU's shard): 8,192 envs, 16 agents, 512x512,
     dist_reward, the bench's 2000-step episodes: the early phase, steps 1..30
     after the reset, where the most maps go to the distance transform's list.
@@ -181,11 +194,12 @@ def test_c5_bench_shape_full_size(torch_cuda):
     reward, the float distance obs layer), every known (max d, witness) of
     them against a fresh transform, invariants over all envs; the steps must
     list maps for the full transform and the top-cell cache must serve some
-    (dec_grid_rl.py:206-258,260-282)."""
+    (dec_grid_rl.py:206-258,260-282).  rank 7: the last shard of C5's
+    65,536 envs (global envs 57,344..65,535)."""
     from marlcov import _lib
     sample = [0, 2600, 5555, 8191]
     env, _, listed, cached = run_full_size(torch_cuda, "c5", 2000, 30, sample, "env_kernel<128,1,u32,C5>",
-                                           inv_every=10, dist_every=3)
+                                           inv_every=10, dist_every=3, rank=rank)
     assert listed > 0 and cached > 0, (listed, cached)
     assert int(env.get_state(_lib.FIELD_CURRSTEP).min()) == 30
 

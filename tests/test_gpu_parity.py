@@ -50,11 +50,12 @@ def test_facade_matches_reference_golden(torch_cuda, name):
 
 @pytest.mark.parametrize("policy", KNOWN_ANSWER_POLICIES)
 def test_facade_known_answer(torch_cuda, policy):
-    """SURVEY 8(c) pin 3, the reference's only published result: the BSA and
-    BA* controllers (Policies/bsa.py:14, Policies/ba_star.py:10) cover 100 %
-    of the hand-made test grids (Utils/gridmaker.py:23-43) with total reward
-    234 (Example_Experiments/Non_Learning/{BSA,BA_Star}/Example/
-    TerminalOutput.txt).  Their recorded test episodes (captured from the
+    """SURVEY 8(c) pin 3: the BSA and BA* controllers (Policies/bsa.py:14,
+    Policies/ba_star.py:10) cover 100 % of the hand-made test grids
+    (Utils/gridmaker.py:23-43; the published result,
+    Example_Experiments/Non_Learning/BA_Star/Example/TerminalOutput.txt:
+    172-173) with total reward 234 (captured by running the reference in the
+    build container, not published).  Their recorded test episodes (captured from the
     reference under the example configs: square sensor r=1,
     single_square_tool, dijkstra_input, egoradius 1) replay through the HIP
     facade with the observation, reward and done of every step equal to the

@@ -49,6 +49,18 @@ def test_struct_layout_and_version(lib):
     assert lib.mc_struct_size(7) == -1
 
 
+def test_build_params(lib):
+    """mc_build_param: the distance transform's build constants (kDistK,
+    kDistT, the row limit) that bench.py prices C5 with."""
+    from marlcov import _lib
+    assert lib.mc_build_param(_lib.PARAM_DIST_CACHE_CELLS) == 512
+    assert lib.mc_build_param(_lib.PARAM_DIST_T) == 20
+    # the transform's row limit (DESIGN.md section 7: bg2_1073x1073 maps, 1,079
+    # extended rows at egoradius 2, are rejected with dist_reward)
+    assert lib.mc_build_param(_lib.PARAM_DIST_MAX_ROWS) == 832
+    assert lib.mc_build_param(99) == -1
+
+
 def _cfg(**kw):
     from marlcov import _lib
     c = _lib.McConfig()
@@ -157,7 +169,7 @@ def test_c5_design_bytes_formula():
     import bench
     f = bench.c5_design_bytes_per_step
     assert f(1, 16, 10, 2, 518, 0, 0, 0, 1) == 15408
-    assert bench.DIST_CACHE_BYTES == 4128
+    assert bench.dist_cache_bytes() == 4128  # kDistK from the library (mc_build_param)
     # 100 listed over 2 launches: 60 served, 40 full transforms
     extra = 40 * (33541 + 4128) + 60 * 4128 + 100 * 4
     assert f(8192, 16, 10, 2, 518, 100, 60, 40, 2) == 8192 * 15408 + extra / 2
@@ -336,3 +348,30 @@ def test_kernel_variant_null_env(lib):
     assert lib.mc_kernel_variant(None) == b""
     assert "null" in lib.mc_last_error().decode()
     assert lib.mc_random_actions(None, 0, 0, None, None) == -1
+
+
+def test_gridload_reference_png_maps(tmp_path):
+    """marlcov.gridload on the reference's own PNG maps (Grids/bg2_100x100,
+    bg2_1073x1073; copies in tests/golden/maps): the grids equal what the
+    reference's gridload produced from the same files
+    (tests/golden/bg2_100x100_stc.npz, gridmaker.py:82-102), values in
+    {-1, 1} from mode-L {0, 255} pixels, the train / test split of two files
+    (train = test = both, :96-98), and sort=True orders by file name."""
+    import shutil
+
+    import marlcov
+    maps = os.path.join(os.path.dirname(__file__), "golden", "maps")
+    for n in os.listdir(maps):
+        if n.startswith("bg2_100x100__"):
+            shutil.copyfile(os.path.join(maps, n), tmp_path / n.split("__", 1)[1])
+    train, test = marlcov.gridload({"grid_dir": str(tmp_path), "numgrids": 30}, sort=True)
+    assert len(train) == len(test) == 2
+    assert all(a is b for a, b in zip(train, test))
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "bg2_100x100_stc.npz"))
+    assert sorted(g.astype(np.int8).tobytes() for g in train) == sorted(g.tobytes() for g in z["test_grids"])
+    big = tmp_path / "big"
+    big.mkdir()
+    shutil.copyfile(os.path.join(maps, "bg2_1073x1073__AR0011SR.png"), big / "AR0011SR.png")
+    train, test = marlcov.gridload({"grid_dir": str(big), "numgrids": 30})
+    assert train == [] and len(test) == 1 and test[0].shape == (1073, 1073)
+    assert set(np.unique(test[0]).tolist()) <= {-1.0, 1.0}

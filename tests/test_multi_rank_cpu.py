@@ -146,3 +146,53 @@ def test_two_rank_sharded_episodes_match_one_batch():
         assert merged[e] == whole[e], e
     # the episodes really ended and restarted inside the run (maxsteps=5)
     assert all(sum(d for _, d, _ in whole[e]) >= 2 for e in whole)
+
+
+# ---------------------------------------------------------------------------
+# 3. bench.py --gpus N starts its own ranks (no torchrun in the command)
+# ---------------------------------------------------------------------------
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+@pytest.mark.parametrize("gpus,config,per_rank", [(2, "c2", 4096), (8, "c2", 4096), (2, "c5", 8192)])
+def test_bench_gpus_flag_launches_ranks(gpus, config, per_rank):
+    """`python bench.py --gpus N` (no torchrun) runs N ranks: rank 0's one
+    line says n_gpus N, the global batch is N x the per-GPU envs (C3 = 8 x
+    4,096, C5 = 8 x 8,192), and every rank's shard starts at its global env
+    offset (the seeds the device streams are keyed by)."""
+    rc, lines, err = _bench(["--gpus", str(gpus), "--dist-backend", "gloo", "--plan", "--config", config])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    plan = lines[0]
+    assert plan["n_gpus"] == gpus and plan["global_envs"] == gpus * per_rank and plan["scaling"] == "weak"
+    assert [p["rank"] for p in plan["plan"]] == list(range(gpus))
+    for r, p in enumerate(plan["plan"]):
+        assert p["env_range"] == [r * per_rank, (r + 1) * per_rank]
+        assert p["seeds"] == shard_seeds(r * per_rank)
+
+
+def test_bench_refuses_world_mismatch():
+    """A world size that differs from --gpus exits non-zero without a line."""
+    rc, lines, err = _bench(["--gpus", "2", "--plan"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines and "WORLD_SIZE=1" in err
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """RCCL ranks need one GPU each: --gpus above the visible count exits
+    non-zero in the launcher, before any rank starts (nothing printed)."""
+    if torch.cuda.device_count() >= 16:
+        pytest.skip("16 GPUs visible")
+    rc, lines, err = _bench(["--gpus", "16", "--steps", "1", "--warmup", "0", "--no-cpu"])
+    assert rc != 0 and not lines and "visible" in err

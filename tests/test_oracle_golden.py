@@ -54,11 +54,37 @@ def test_golden_inventory():
 
 @pytest.mark.parametrize("policy", KNOWN_ANSWER_POLICIES)
 def test_oracle_known_answer(policy):
-    """SURVEY 8(c) pin 3, the reference's published result: BSA / BA* cover
-    100 % of every hand-made test grid with total reward 234
-    (Example_Experiments/Non_Learning/{BSA,BA_Star}/Example/TerminalOutput.txt).
-    The recorded controller trajectories replay bit-exactly on the oracle."""
+    """SURVEY 8(c) pin 3: BSA / BA* cover 100 % of every hand-made test grid
+    (the published result, Example_Experiments/Non_Learning/BA_Star/Example/
+    TerminalOutput.txt:172-173) with total reward 234 (captured by running
+    the reference here, make_known_answer.py; not a published number).  The
+    recorded controller trajectories replay bit-exactly on the oracle."""
     ka = load_known_answer()
     res = replay_known_answer(DecGridRLRef, ka, policy)
     assert len(res) == 12 and all(r == (234.0, 1.0) for r in res)
     assert sorted(set(ka[policy + "__ep_grid"].tolist())) == [0, 1, 2]
+
+
+def test_oracle_bg2_stc_replay():
+    """The reference's own shipped maps (Grids/bg2_100x100, the STC example
+    config, Example_Experiments/Non_Learning/STC/Example/config.json): the
+    STC controller's test episodes captured from the reference
+    (tests/golden/make_bg2_golden.py) replay bit-exactly on the oracle --
+    observation, reward and done every step, then the recorded total reward
+    and percent_covered().  The grids the reference's gridload produced equal
+    the package's PNG loader on the same files."""
+    import os
+
+    from marlcov import gridload
+    ka = load_known_answer("bg2_100x100_stc.npz")
+    tmp = os.path.join(GOLDEN_DIR, "maps")
+    names = sorted(n for n in os.listdir(tmp) if n.startswith("bg2_100x100__"))
+    grids = []
+    from PIL import Image
+    for n in names:
+        img = np.array(Image.open(os.path.join(tmp, n))).astype(float)
+        grids.append(np.clip(img - 1, -1, 1))
+    stored = [g.astype(np.float64) for g in ka["test_grids"]]
+    assert sorted(g.tobytes() for g in grids) == sorted(g.tobytes() for g in stored)
+    res = replay_known_answer(DecGridRLRef, ka, "stc", expect=None)
+    assert len(res) == 4 and int(ka["stc__ep_len"].sum()) > 2000
