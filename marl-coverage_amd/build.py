@@ -19,9 +19,14 @@ OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "libmarlcov.so")
 ARCH = os.environ.get("MARLCOV_ARCH", "gfx950")
 
-# No -ffast-math / -ffp-contract=fast: the lidar march and reward assembly
-# must keep the reference's IEEE float64 adds and correctly rounded division.
-CFLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+# No -ffast-math, and contraction explicitly off (hipcc's device default is
+# -ffp-contract=fast-honor-pragmas, which may fuse a multiply and an add into
+# an FMA): the lidar march, the reward assembly and the float32 distance
+# terms must keep the reference's separately rounded IEEE operations
+# (NumPy never fuses).  The minimap's bilinear weights additionally use
+# __dmul_rn / __dadd_rn (mc_minimap.hip), which no flag can fuse.
+CFLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
+          "-Wno-unused-function"]
 
 
 def sources():

@@ -433,12 +433,13 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     const char* dc = getenv("MARLCOV_DIST_CACHE");
     if (!c.map_sharing && !(dc && dc[0] == '0')) {
       void *cc = nullptr, *cd = nullptr, *ch = nullptr, *sm = nullptr;
-      void *gk = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr, *pc = nullptr, *rm = nullptr;
+      void *gk = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr, *pc = nullptr, *rm = nullptr, *go = nullptr;
       const size_t maps = (size_t)s.B * s.N;
       if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
           dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess ||
           dev_alloc(E, &sm, maps * mc::kDistStrips * 4) != MC_OK || dev_alloc(E, &gk, maps * 8) != MC_OK ||
           dev_alloc(E, &gc, (size_t)mc::kDistGSlots * 4) != MC_OK || dev_alloc(E, &pc, maps * 4) != MC_OK ||
+          dev_alloc(E, &go, (size_t)mc::kDistGSlots * 4) != MC_OK ||
           dev_alloc(E, &rm, maps * 8) != MC_OK ||
           dev_alloc(E, &ga, (size_t)mc::kDistGSlots * 4 * mc::kDistK * 8) != MC_OK ||
           dev_alloc(E, &fl, (maps * 2 + 8) * 4) != MC_OK) {
@@ -454,6 +455,7 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       E->s.dist_rmask = (unsigned long long*)rm;
       E->s.dist_gkey = (unsigned long long*)gk;
       E->s.dist_gcnt = (uint32_t*)gc;
+      E->s.dist_govf = (uint32_t*)go;
       E->s.dist_gcand = (int2*)ga;
       // MARLCOV_DIST_SPLIT=0: every listed map's full transform in one workgroup
       const char* sp = getenv("MARLCOV_DIST_SPLIT");

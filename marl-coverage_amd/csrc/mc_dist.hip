@@ -567,6 +567,28 @@ constexpr bool kXcdParts = MC_DIST_XCD != 0;
 #define MC_DIST_BALANCE 1
 #endif
 constexpr bool kBalance = MC_DIST_BALANCE != 0;
+#ifndef MC_DIST_OPAQUE_TID  // build knob (A/B): 0 = round 5's item loop (VGPR spills at <17>)
+#define MC_DIST_OPAQUE_TID 1
+#endif
+#ifndef MC_DIST_ACQREL  // build knob (A/B): 0 = round 5's relaxed arrival add (ordering by vmcnt + sc1 only)
+#define MC_DIST_ACQREL 1
+#endif
+#ifndef MC_DIST_PARTLIST  // build knob (A/B): 1 = part lists (below); off: measured slower, round 6
+#define MC_DIST_PARTLIST 0
+#endif
+// Part lists: a split map without a cache bound (theta0 = 0, e.g. every map
+// early after a reset) -- each part collects its own cells with d >= its own
+// maximum - kDistT (a superset of its cells with d >= M - kDistT, M >= that
+// maximum) and publishes them like the one-pass candidates; a part whose
+// maximum is below the best published key - kDistT holds no cache cell and
+// skips it.  The merger then needs the serial cache pass only when a part
+// that overflowed its list reaches M - kDistT (State::dist_govf).
+// Measured slower (round 6, profiles/r6/dist/: C5 default window 162.5 vs
+// 158.0 us per step, steady 150.8 vs 147.0): the parts' extra strip passes
+// cost more than the merger's serial pass they save.  Kept as an A/B knob,
+// parity-tested (tests/test_gpu_shapes.py, 8 envs: the mass reset splits
+// every map with theta0 = 0).
+constexpr bool kPartList = MC_DIST_PARTLIST != 0 && kOnePass;
 
 // The strips a full transform of map ea runs with the lower bound theta of
 // its new max(d) (bit st; the rest are pruned, dist_kernel_t's strip loop):
@@ -606,6 +628,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   __shared__ int s_ccount;
   __shared__ int s_kept;
   __shared__ uint32_t s_base;
+  __shared__ int s_lb;
   __shared__ int s_smax[kMaxTrack];
   __shared__ int32_t s_ccell[kDistK];
   __shared__ uint16_t s_cdv[kDistK];  // d < 0xFFFF (the transform saturates there)
@@ -662,6 +685,14 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     count[3] = 0;
   }
   for (uint32_t it = blockIdx.x; it < n_items; it += (strided ? gridDim.x : n_items)) {
+    // the thread index, opaque per item: otherwise the compiler hoists every
+    // per-thread address and lane mask of the item body out of the item loop
+    // and keeps them live across it -- 24 VGPRs spilled to scratch (100 B per
+    // lane, ~24 MB of scratch writes per C5 step) at <17>, none with this
+    int tid = threadIdx.x;
+#if MC_DIST_OPAQUE_TID
+    asm volatile("" : "+v"(tid));
+#endif
     // modes 2 / 3: the full-list entry (and mode 2's part)
     const uint32_t l = it >> 3;
     const uint32_t fi = mode == 2 ? (xcd ? (l / (uint32_t)S) * 8u + (it & 7u) : it / (uint32_t)S) : (mode == 3 ? it : 0u);
@@ -718,6 +749,15 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       s_kept = 0;
     }
     for (int i = tid; i < kMaxTrack; i += kDtThreads) s_smax[i] = 0;
+    // every wave sees the scalars above before it reads one: s_fkey is read
+    // for theta0 below even when no cache try (whose barriers would order it)
+    // runs.  (Round 5's intermittent split/unsplit dist_obs mismatch at the
+    // mass auto-reset of test_c5_unsplit_transform_is_identical: with no map
+    // cached, waves of the unsplit path read the previous workgroup's s_fkey
+    // out of LDS before thread 0 zeroed it, took its d as theta0, pruned
+    // strips the other waves ran, and fell out of step at the strips'
+    // barriers.)
+    __syncthreads();
     // the map's top-cell cache (mc_internal.h State::dist_ch)
     int ccnt = -1, cM0 = 0, bx0 = 0, by0 = 0, bx1 = -1, by1 = -1;
     if (s.dist_ch) {
@@ -731,9 +771,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       by1 = h1.y;
     }
     // ---- the top-cell cache fast path (cache_try) for a listed map
-    bool fast = false;
+    bool fast = false, tried = false;
     if (mode < 2 && list != nullptr && ccnt > 0) {
-      bool tried = false;
       cache_try<kDtThreads>(s, pad, T, px, py, free_t, ccnt, bx0, by0, bx1, by1, reinterpret_cast<uint64_t*>(G),
                             s.dist_cc + (size_t)ea * kDistK, s.dist_cd + (size_t)ea * kDistK, s_cdv, s_d, &s_fkey,
                             &s_ffail, tried);
@@ -743,7 +782,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     DSTAMP(tsf);
     // the exact current d of the cached cells (the fast path computed them
     // before it failed): a lower bound of the new max(d)
-    const int theta0 = mode >= 2 ? (int)full[9 + 2 * fi] : ((s.dist_ch && list != nullptr) ? (int)(s_fkey >> 16) : 0);
+    // (a try that returned before staging -- box too large -- leaves none)
+    const int theta0 = mode >= 2 ? (int)full[9 + 2 * fi] : (tried ? (int)(s_fkey >> 16) : 0);
     bool need_cb = true;  // the map's bitboard in LDS
     // ---- merge a split map's parts' partials: the best key, the raw target
     // d (in the output buffers), the strip maxima, the cache candidates.
@@ -753,10 +793,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       __syncthreads();  // the item's LDS scalars are initialised; every thread is past its own list
       if (tid == 0) s_ccount = 0;
       __syncthreads();
-      // the parts' candidates: a one-pass list (with theta0), else none
-      const uint32_t total = (kOnePass && theta0 > 0) ? ld_ho(s.dist_gcnt + fi, sc1) : 0u;
+      // the parts' candidates: a one-pass list (with theta0), the part lists
+      // (without), else none
+      const uint32_t total = ((kOnePass && theta0 > 0) || kPartList) ? ld_ho(s.dist_gcnt + fi, sc1) : 0u;
       const unsigned long long gk = ld_ho(s.dist_gkey + ea, sc1);
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
+      // a part list that overflowed and may hold cache cells: the serial pass
+      const uint32_t ovf = (kPartList && theta0 == 0) ? ld_ho(s.dist_govf + fi, sc1) : 0u;
       for (int t = tid; t < T; t += kDtThreads)
         s_d[t] = (int)(t < 5 ? ld_ho(pre_out + (size_t)ea * 8 + 1 + t, sc1)
                              : ld_ho(dist_obs + (size_t)ea * E * E + (t - 5), sc1));
@@ -778,14 +821,16 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         s_key = gk;
         s_cov = gk != 0;  // a covered map's key is nonzero (its far or cell field)
         if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
+        if (ovf > 0u && (int)ovf - 1 >= thr) s_ccount = kDistK + 1;
         s.dist_gkey[ea] = 0;  // zero for the map's next split transform
         s.dist_gcnt[fi] = 0;
+        if (kPartList) s.dist_govf[fi] = 0;
       }
       __syncthreads();
     };
     if (mode == 3) {
       merge_parts(false);
-      need_cb = s_cov && !(kOnePass && theta0 > 0 && s_ccount <= kDistK);  // the second pass
+      need_cb = s_cov && !(((kOnePass && theta0 > 0) || kPartList) && s_ccount <= kDistK);  // the second pass
     }
     if (!fast && need_cb) {
       if (mode != 3)  // (mode 3 holds the parts' targets)
@@ -1137,7 +1182,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       }
       ran |= 1ull << (st < 64 ? st : 63);
-      strip(st, -1, (kOnePass && theta0 > 0) ? max(theta0, runmax) - kDistT : -1);
+      // (a bound below kDistT: every cell is a candidate, d >= 0 -- the list
+      // then overflows and the cache pass runs; a negative threshold would
+      // collect nothing and leave the list short)
+      strip(st, -1, (kOnePass && theta0 > 0) ? max(max(theta0, runmax) - kDistT, 0) : -1);
     }
     DSTAMP(ts2);
     const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
@@ -1165,9 +1213,38 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
         if ((ran >> st) & 1ull) st_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, (uint32_t)min(s_smax[st], 0xFFFF), kFused);
-      if (kOnePass && theta0 > 0) {
+      bool part_list = false;  // this part collected its own candidates (theta0 = 0)
+      if (kPartList && theta0 == 0 && s.dist_ch) {
+        // the part's own maximum and the best key the parts published so far
+        // (a lower bound of M): below it by more than kDistT, no cache cell
+        if (tid == 0) {
+          const unsigned long long g = __hip_atomic_load((g_u64*)(s.dist_gkey + ea), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+          s_lb = (int)(max(g, (unsigned long long)s_key) >> 48);
+          s_ccount = 0;
+        }
+        __syncthreads();
+        const int pm = s_key ? (int)(s_key >> 48) : -1;
+        if (pm >= 0 && pm >= s_lb - kDistT) {
+          part_list = true;
+          const int thr = max(pm - kDistT, 0);
+          carry_in(st_lo);
+          for (int st = st_lo; st < st_hi; ++st) {
+            if (st >= kMaxTrack || s_smax[st] >= thr) {
+              strip(st, thr, -1);
+              __syncthreads();
+              if (s_ccount > kDistK) break;  // overflowed: the merger's pass if it matters
+            } else {
+              carry_over(st);
+            }
+          }
+          __syncthreads();
+          if (tid == 0 && s_ccount > kDistK) atomicMax(s.dist_govf + fi, (uint32_t)pm + 1u);
+        }
+      }
+      if ((kOnePass && theta0 > 0) || part_list) {
         const int n = s_ccount;
-        if (n > 0) {
+        if (n > 0 && (n <= kDistK || theta0 > 0)) {
           if (tid == 0) s_base = atomicAdd(s.dist_gcnt + fi, (uint32_t)(n <= kDistK ? n : kGCand + 1));
           __syncthreads();
           const uint32_t base = s_base;
@@ -1178,15 +1255,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         }
       }
       if constexpr (kFused) {
-        // every storing wave's stores done, then one arrival per part; the
-        // last to arrive merges (its own loads wait for its add, the other
-        // waves for the barrier after it)
+        // every storing wave's stores done, then one arrival per part: an
+        // agent-scope acq_rel add (release: the part's published words are
+        // visible at agent scope before the count moves -- buffer_wbl2 of the
+        // XCD's L2 after the waves' stores have completed; acquire: the
+        // merger's loads after it miss its L1 / L2, buffer_inv).  The last
+        // to arrive merges (its other waves read after the barrier)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) s_base = atomicAdd(s.dist_pcnt + ea, 1u);
+        if (tid == 0)
+          s_base = MC_DIST_ACQREL ? __hip_atomic_fetch_add(s.dist_pcnt + ea, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                                  : atomicAdd(s.dist_pcnt + ea, 1u);
         __syncthreads();
         merged = s_base == (uint32_t)S - 1u;
-        if (merged && tid == 0) s.dist_pcnt[ea] = 0;  // zero for the map's next split transform
+        if (merged && tid == 0)  // zero for the map's next split transform
+          __hip_atomic_store(s.dist_pcnt + ea, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (merged) {
         // the map's bitboard is staged here (every part stages it): a second
@@ -1203,8 +1286,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
             return d < 0xFFFFull ? d : 0xFFFFull;
           };
           s.stamps[ea] = f16(ts0, ts1) | (f16(ts1, ts2) << 16) | (f16(ts2, tp) << 32) | (1ull << 52);
-          // per part (tools/dist_stamps.py allocates B*16 + 8192 entries):
-          // stage, strips, publish, strips run, S, merged
+          // per part (items it < 4096; the highest index written is
+          // B*16 + 20480 + 4095, so a stamps buffer needs B*16 + 24576
+          // entries, as tools/dist_stamps.py allocates): stage, strips,
+          // publish, strips run, S, merged
           if (it < 4096u) {  // absolute: workgroup start, item start, part end (merged: below)
             s.stamps[(size_t)s.B * 16u + 12288u + it] = ts0;
             s.stamps[(size_t)s.B * 16u + 16384u + it] = tp;
@@ -1241,7 +1326,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         // reaches it; the others only carry their last covered column)
         int cnt = -1;
         // the main pass's list (mode 3: the parts' lists) holds them all
-        const bool main_ok = kOnePass && theta0 > 0 && s_ccount <= kDistK;
+        // (mode 3 / a fused merger of a map without theta0: the part lists)
+        const bool parts = mode == 3 || (mode == 2 && S > 1);
+        const bool main_ok = kOnePass && (theta0 > 0 || (kPartList && parts)) && s_ccount <= kDistK;
         if (cov && M >= 0 && main_ok) {
           const int thr = M - kDistT, n = s_ccount;
           for (int k = tid; k < n; k += kDtThreads)

@@ -156,6 +156,10 @@ struct State {
   // [kDistGSlots][4 * kDistK] (cell, d)
   unsigned long long* dist_gkey;
   uint32_t* dist_gcnt;
+  // by full-list index: 1 + the largest own maximum of the parts whose
+  // candidate list overflowed (0: none), for maps split without a cache
+  // bound (theta0 = 0; mc_dist.hip part lists)
+  uint32_t* dist_govf;
   int2* dist_gcand;
   uint32_t* dist_pcnt;  // [B][N] parts of a split map done this launch (mode 2 fused; zero between uses)
   // [B][N] the strips a listed map's split transform runs (bit st: not

@@ -38,7 +38,7 @@ def _actions(rs, B, N, sentinel_p=0.05, noop_p=0.06):
     return acts
 
 
-def run_against_oracle(torch, env, cfg, rs, T, envs, seed, label, dist_check=False, sentinel_p=0.05):
+def run_against_oracle(torch, env, cfg, rs, T, envs, seed, label, dist_check=False, sentinel_p=0.05, on_step=None):
     """Step ``env`` T times with random actions (no-op codes and sentinel rows
     included) and compare the envs in ``envs`` with oracle envs rebuilt from
     the device state after the reset: reward, done, obs (with the float dist
@@ -73,6 +73,8 @@ def run_against_oracle(torch, env, cfg, rs, T, envs, seed, label, dist_check=Fal
             compare_env(st, b, refs[b], tag)
         if dist_check:
             check_dist_mw(env, refs, f"{label} t={t}", envs=envs)
+        if on_step is not None:
+            on_step(t)
     env.check()
     return resets
 
@@ -466,3 +468,77 @@ def test_shards_reproduce_one_batch(torch_cuda):
     assert int(whole.get_state(_lib.FIELD_EPISODE).min()) >= 5  # maxsteps 9 over 50 steps
     for e in (whole, lo, hi):
         e.check()
+
+
+@pytest.mark.parametrize("B", [64, 8])
+def test_c5_split_maps_across_auto_reset_match_oracle(torch_cuda, B):
+    """C5 geometry (16 agents, 512 x 512, dist_reward) across the first
+    auto-reset: B envs, maxsteps 50, two envs tracked by the oracle from the
+    reset through step 55 (reward with the float32 distance terms, the float
+    distance obs layer, maps; every known (max d, witness) against a fresh
+    transform).  The steps before the reset split their few full transforms
+    over parts (<= 256 maps on the full list); step 50 resets every map at
+    once (all caches dropped, B x 16 maps listed).  B = 64: 1,024 maps, one
+    workgroup each; B = 8: 128 maps split over parts with no cache bound
+    (theta0 = 0: the part lists, and their merge).
+    dec_grid_rl.py:222-223,239-240,260-282,449-531."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=50)
+    env = marlcov.BatchCoverageEnv(cfg, B, gen=dict(width=512, length=512, prob_obst=0.1, seed=1001),
+                                   seed=9, auto_reset=True)
+    assert ",C5>" in env.kernel_variant(), env.kernel_variant()
+    env.reset()
+    tot = [env.get_state(_lib.FIELD_DIST_TOTALS).cpu().tolist()]
+    fulls = []  # maps fully transformed per step (MC_FIELD_DIST_TOTALS deltas)
+
+    def on_step(t):
+        tot.append(env.get_state(_lib.FIELD_DIST_TOTALS).cpu().tolist())
+        fulls.append(tot[-1][2] - tot[-2][2])
+    resets = run_against_oracle(torch, env, cfg, np.random.RandomState(55), 55, [1, B - 2], 9, f"c5 reset B={B}",
+                                dist_check=True, sentinel_p=0.0, on_step=on_step)
+    assert resets == 2  # both tracked envs reset at step 50, once
+    assert int(env.get_state(_lib.FIELD_CURRSTEP).max()) == 5
+    msg = " ".join(map(str, fulls))
+    assert fulls[49] == 16 * B, msg  # step 50: the mass reset sends every map to the full transform
+    if B == 64:
+        assert any(0 < f <= 256 for f in fulls[:49]), msg  # split steps before it
+    else:
+        assert all(f <= 256 for f in fulls), msg  # every full transform split, the reset's too
+
+
+def test_dist_totals_bookkeeping(torch_cuda, monkeypatch):
+    """MC_FIELD_DIST_TOTALS (the counters bench.py prices C5's design bytes
+    with): over K steps, launches == K, listed == served + full, and listed
+    equals the sum of the per-step MC_FIELD_DIST_LISTED values -- with the
+    split path (cache tries + split transforms) and with MARLCOV_DIST_SPLIT=0
+    (one workgroup per listed map); both paths count the same maps."""
+    import marlcov
+    from marlcov import _lib
+    torch = torch_cuda
+    cfg = base_cfg(numrobot=16, dist_reward=1, maxsteps=2000)
+    res = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("MARLCOV_DIST_SPLIT", split)
+        env = marlcov.BatchCoverageEnv(cfg, 32, gen=dict(width=512, length=512, prob_obst=0.1, seed=77),
+                                       seed=4, auto_reset=True)
+        env.reset()
+        for t in range(40):  # past the early phase's densest lists
+            env.step(env.random_actions(8, t))
+        t0 = env.get_state(_lib.FIELD_DIST_TOTALS).cpu().tolist()
+        listed = served = 0
+        K = 30
+        for t in range(40, 40 + K):
+            env.step(env.random_actions(8, t))
+            listed += int(env.get_state(_lib.FIELD_DIST_LISTED).item())
+            served += int(env.get_state(_lib.FIELD_DIST_CACHED).item())
+        t1 = env.get_state(_lib.FIELD_DIST_TOTALS).cpu().tolist()
+        d = [b - a for a, b in zip(t0, t1)]
+        assert d[3] == K, (split, d)
+        assert d[0] == d[1] + d[2], (split, d)
+        assert d[0] == listed and d[1] == served, (split, d, listed, served)
+        assert d[0] > 0, d
+        res[split] = d[0]
+        del env
+    assert res["1"] == res["0"], res  # the same maps listed either way

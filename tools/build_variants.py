@@ -18,7 +18,7 @@ def build(spec):
     name, _, flags = spec.partition(":")
     out = os.path.join(PKG, f"libmarlcov_v_{name}.so")
     srcs = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")))
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off", "-shared",
            *flags.split(), "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc"),
            "-o", out, *srcs]
     subprocess.run(cmd, check=True)
