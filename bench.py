@@ -520,7 +520,13 @@ def launch_ranks(args):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
     sys.stdout.flush()
-    return subprocess.call(cmd)
+    # relay rank 0's JSON line on stdout, line by line as it comes; anything
+    # else the ranks print there (gloo's connection messages) goes to stderr
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    return p.wait()
 
 
 def print_plan(args, world, rank, e0, e1, total_envs, scaling):

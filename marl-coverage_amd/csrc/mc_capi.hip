@@ -35,6 +35,7 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
 size_t dist_lds_bytes(const State& s, int pad);
 size_t dist_static_lds_bytes();
 int dist_max_rows();
+int dist_cache_max_rows();
 size_t dijkstra_lds_bytes(const State& s, int pad);
 hipError_t launch_minimap(const State& s, int mini, double* out, hipStream_t stream);
 __global__ void dijkstra_kernel(State s, int pad, int layer, int Lc, uint8_t* obs_out,
@@ -431,7 +432,9 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
     // maps add cells outside the agent's own sensing windows) or
     // MARLCOV_DIST_CACHE=0
     const char* dc = getenv("MARLCOV_DIST_CACHE");
-    if (!c.map_sharing && !(dc && dc[0] == '0')) {
+    // and off for maps past the LDS-bitboard transform's rows (the big-map
+    // kernel transforms every listed map whole, mc_dist.hip)
+    if (!c.map_sharing && !(dc && dc[0] == '0') && s.Wp + 2 * c.pad <= mc::dist_cache_max_rows()) {
       void *cc = nullptr, *cd = nullptr, *ch = nullptr, *sm = nullptr;
       void *gk = nullptr, *gc = nullptr, *ga = nullptr, *fl = nullptr, *pc = nullptr, *rm = nullptr, *go = nullptr;
       const size_t maps = (size_t)s.B * s.N;

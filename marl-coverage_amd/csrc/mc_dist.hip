@@ -99,6 +99,16 @@ constexpr u16x2 kNone2 = {0xFFFF, 0xFFFF};
 constexpr u16x2 kRowOff2 = {kRowOff, kRowOff};
 __device__ __forceinline__ u16x2 splat2(int v) { return u16x2{(uint16_t)v, (uint16_t)v}; }
 
+// The thread index as an opaque value: the compiler can neither hoist what
+// is derived from it out of the item loops nor keep it live across them (it
+// hoisted every per-thread address and lane mask of an item out of
+// dist_kernel_t's item loop and spilled them: 24 VGPRs at <17>, round 5)
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // Packed minima across the 32 chunks of a column pair (lane c of a half wave
 // = chunk c): over the chunks before this one / after it (0xFFFF: none).
 // DPP row shifts inside each 16-lane row, the other row's total by readlane.
@@ -109,7 +119,7 @@ __device__ __forceinline__ u16x2 dpp2(u16x2 v) {  // source lane out of the row:
 }
 // 64 chunks (1024 threads): the whole wave, four 16-lane rows
 __device__ __forceinline__ u16x2 excl_prefix_min64(u16x2 v) {
-  const int l = threadIdx.x & 63;
+  const int l = opaque_tid() & 63;
   u16x2 x = __builtin_elementwise_min(v, dpp2<0x111>(v));
   x = __builtin_elementwise_min(x, dpp2<0x112>(x));
   x = __builtin_elementwise_min(x, dpp2<0x114>(x));
@@ -125,7 +135,7 @@ __device__ __forceinline__ u16x2 excl_prefix_min64(u16x2 v) {
   return __builtin_elementwise_min(e, carry);
 }
 __device__ __forceinline__ u16x2 excl_suffix_min64(u16x2 v) {
-  const int l = threadIdx.x & 63;
+  const int l = opaque_tid() & 63;
   u16x2 x = __builtin_elementwise_min(v, dpp2<0x101>(v));
   x = __builtin_elementwise_min(x, dpp2<0x102>(x));
   x = __builtin_elementwise_min(x, dpp2<0x104>(x));
@@ -141,7 +151,7 @@ __device__ __forceinline__ u16x2 excl_suffix_min64(u16x2 v) {
   return __builtin_elementwise_min(e, carry);
 }
 __device__ __forceinline__ u16x2 excl_prefix_min32(u16x2 v) {
-  const int l = threadIdx.x & 63;
+  const int l = opaque_tid() & 63;
   u16x2 x = __builtin_elementwise_min(v, dpp2<0x111>(v));  // row_shr:1
   x = __builtin_elementwise_min(x, dpp2<0x112>(x));        // row_shr:2
   x = __builtin_elementwise_min(x, dpp2<0x114>(x));        // row_shr:4
@@ -154,7 +164,7 @@ __device__ __forceinline__ u16x2 excl_prefix_min32(u16x2 v) {
   return __builtin_elementwise_min(e, carry);
 }
 __device__ __forceinline__ u16x2 excl_suffix_min32(u16x2 v) {
-  const int l = threadIdx.x & 63;
+  const int l = opaque_tid() & 63;
   u16x2 x = __builtin_elementwise_min(v, dpp2<0x101>(v));  // row_shl:1
   x = __builtin_elementwise_min(x, dpp2<0x102>(x));        // row_shl:2
   x = __builtin_elementwise_min(x, dpp2<0x104>(x));        // row_shl:4
@@ -311,7 +321,7 @@ __device__ __forceinline__ void cache_try(const State& s, int pad, int T, int px
                                           const int32_t* cc, const int32_t* cd, uint16_t* cdv, int* s_d,
                                           uint32_t* fkey, int* ffail, bool& tried, uint32_t* span = nullptr,
                                           uint64_t* ts = nullptr) {
-  const int tid = threadIdx.x, E = s.E;
+  const int tid = opaque_tid(), E = s.E;
   const int ti0 = bx0 >> 3, ti1 = bx1 >> 3, tj0 = by0 >> 3, tj1 = by1 >> 3;  // floor
   const int nbr = bx1 >= bx0 ? ti1 - ti0 + 1 : 0, nbc = by1 >= by0 ? tj1 - tj0 + 1 : 0;
   const int nt = nbr * nbc;
@@ -507,7 +517,7 @@ template <int NTH>
 __device__ __forceinline__ void cache_serve(const State& s, int T, uint32_t ea, uint32_t fkey, int ccnt, int cM0,
                                             const uint16_t* cdv, const int* s_d, float* pre_out, float* dist_obs,
                                             uint32_t* count) {
-  const int tid = threadIdx.x, E = s.E;
+  const int tid = opaque_tid(), E = s.E;
   const int M = (int)(fkey >> 16), kb = (int)(fkey & 0xFFFFu);
   const float Mf = (float)M;
   if (tid == 0) {
@@ -689,9 +699,10 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // per-thread address and lane mask of the item body out of the item loop
     // and keeps them live across it -- 24 VGPRs spilled to scratch (100 B per
     // lane, ~24 MB of scratch writes per C5 step) at <17>, none with this
-    int tid = threadIdx.x;
 #if MC_DIST_OPAQUE_TID
-    asm volatile("" : "+v"(tid));
+    const int tid = opaque_tid();
+#else
+    const int tid = threadIdx.x;
 #endif
     // modes 2 / 3: the full-list entry (and mode 2's part)
     const uint32_t l = it >> 3;
@@ -1437,11 +1448,6 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
   }
 }
 
-size_t dist_lds_bytes(const State& s, int pad) {
-  return dt_lds(s.Wp + 2 * pad, s.Lp + 2 * pad, s.MT, 5 + s.E * s.E).total;
-}
-
-int dist_max_rows() { return kMaxRows; }
 
 // static LDS of dist_kernel_t beyond dist_lds_bytes: the top-cell cache list
 // (kDistK cells and d), the strip maxima and the scalars
@@ -1577,11 +1583,15 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
 }
 
 // the instantiation whose register chunk holds ceil(RX / kChunks) rows
+static hipError_t launch_big(const State& s, int pad, int post, float* pre_out, float* dist_obs,
+                             const uint32_t* list, uint32_t* count, unsigned grid, hipStream_t stream);
+
 static hipError_t launch_full(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                               const uint32_t* list, uint32_t* count, unsigned grid, int mode, uint32_t* full,
                               hipStream_t stream) {
   const int RX = s.Wp + 2 * pad, cl = chunk_rows(RX);
-  const size_t lds = dist_lds_bytes(s, pad);
+  if (RX > kMaxRows) return launch_big(s, pad, post, pre_out, dist_obs, list, count, grid, stream);
+  const size_t lds = dt_lds(RX, s.Lp + 2 * pad, s.MT, 5 + s.E * s.E).total;
 #define MC_DT(CL)                                                                              \
   do {                                                                                         \
     if (lds > 65536) {                                                                         \
@@ -1604,6 +1614,361 @@ static hipError_t launch_full(const State& s, int pad, int post, float* pre_out,
 #undef MC_DT
   return hipGetLastError();
 }
+
+// --------------------------------------------------------------------------
+// Big maps: extended grids past kMaxRows rows (the reference's own
+// Grids/bg2_1073x1073, 1,079 extended rows at egoradius 2).  The transform
+// above keeps the map's row bitboard in LDS (RX x RW words: 147 KB at 1079 x
+// 1079) next to its strip; a big map's bitboard does not fit beside the
+// strip, so this kernel keeps only two 64-column word columns of the map in
+// LDS at a time and, per row and word column, the first covered column at or
+// right of it (`nxt`, built right to left first: the row pass's nearest
+// covered cell right of a strip).  Same strips, same row and column passes
+// (a wave of 64 row chunks per column pair), same outputs as mode 0 of
+// dist_kernel_t without the top-cell cache (mc_create leaves the cache off
+// for these maps).  One workgroup of 1,024 threads per listed map (or per map
+// with list == nullptr), one per CU (LDS).
+// --------------------------------------------------------------------------
+constexpr int kBigThreads = 1024;
+constexpr int kBigCh = 64;                    // row chunks per column pair: one wave
+constexpr int kBigCL = 17;                    // rows per chunk
+constexpr int kBigSP = 34;                    // strip row stride (u16; 17 dwords: distinct banks)
+constexpr int kBigMaxRows = kBigCh * kBigCL;  // 1,088 extended rows
+
+struct BigLds {
+  size_t nxt, wc, strip, tgt, total;
+};
+__host__ __device__ inline BigLds big_lds(int Wp, int TC, int T) {
+  BigLds L;
+  const int RWm = (TC + 7) >> 3;  // u64 words per map row
+  L.nxt = (((size_t)(RWm + 1) * Wp * 2) + 15) & ~(size_t)15;
+  L.wc = (size_t)2 * Wp * 8;
+  L.strip = (size_t)kBigCh * kBigCL * kBigSP * 2;
+  L.tgt = ((size_t)T * 4 + 15) & ~(size_t)15;
+  L.total = L.nxt + L.wc + L.strip + L.tgt;
+  return L;
+}
+
+// word column q of the map (u64 per map row: columns 64 q .. 64 q + 63) into
+// wc[X], X < Wp: a thread per tile row loads its 8 tiles (two 16-byte pairs of
+// block rows) and transposes their bytes into the 8 row words (v_perm, as the
+// staging above).  q outside the map: zero words.
+__device__ __forceinline__ void big_stage_word(const State& s, const uint64_t* free_t, int q, uint64_t* wc) {
+  const int RWm = (s.TC + 7) >> 3;
+  for (int ti = opaque_tid(); ti < s.TR; ti += kBigThreads) {
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const int tj = 8 * q + j;
+      uint4 t = make_uint4(0u, 0u, 0u, 0u);
+      if (q >= 0 && q < RWm && tj < s.TC) t = *reinterpret_cast<const uint4*>(free_t + tile_index(s.TCS, ti, tj));
+      if (tj + 1 >= s.TC) t.z = t.w = 0u;
+      lo[j] = t.x;
+      hi[j] = t.y;
+      lo[j + 1] = t.z;
+      hi[j + 1] = t.w;
+    }
+    const int nr = min(8, s.Wp - 8 * ti);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (r >= nr) break;
+      const uint32_t* src = r < 4 ? lo : hi;
+      const uint32_t b = (uint32_t)(r & 3);
+      const uint32_t sel2 = b | ((4u + b) << 8) | 0x0C0C0000u;
+      const uint32_t p01 = __builtin_amdgcn_perm(src[1], src[0], sel2);
+      const uint32_t p23 = __builtin_amdgcn_perm(src[3], src[2], sel2);
+      const uint32_t p45 = __builtin_amdgcn_perm(src[5], src[4], sel2);
+      const uint32_t p67 = __builtin_amdgcn_perm(src[7], src[6], sel2);
+      const uint32_t wlo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+      const uint32_t whi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
+      wc[8 * ti + r] = (uint64_t)wlo | ((uint64_t)whi << 32);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBigThreads, 1) void dist_big_kernel(State s, int pad, int post, float* __restrict__ pre_out,
+                                                                 float* __restrict__ dist_obs,
+                                                                 const uint32_t* __restrict__ list,
+                                                                 uint32_t* __restrict__ count) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ unsigned long long s_key;
+  __shared__ int s_cov;
+  const int RX = s.Wp + 2 * pad, RY = s.Lp + 2 * pad;
+  const int RWm = (s.TC + 7) >> 3;
+  const int E = s.E;
+  const int T = post ? 5 + E * E : 5;
+  const BigLds LL = big_lds(s.Wp, s.TC, 5 + E * E);
+  uint16_t* nxt = reinterpret_cast<uint16_t*>(smem);  // [RWm + 1][Wp]: first covered column >= 64 q (0xFFFF: none)
+  uint64_t* wc = reinterpret_cast<uint64_t*>(smem + LL.nxt);  // two word columns [2][Wp]
+  uint16_t* G = reinterpret_cast<uint16_t*>(smem + LL.nxt + LL.wc);  // [kBigCh * kBigCL][kBigSP]
+  int* s_d = reinterpret_cast<int*>(smem + LL.nxt + LL.wc + LL.strip);
+  const int nst = (RY + kStrip - 1) / kStrip;
+  ListView lv;
+  lv.pre[kListShards] = 0;
+  if (list) lv = list_view(s);
+  const uint32_t n_items = list ? lv.pre[kListShards] : (uint32_t)gridDim.x;
+  for (uint32_t it = blockIdx.x; it < n_items; it += (list ? gridDim.x : n_items)) {
+    const int tid = opaque_tid();
+    const uint32_t ea = list ? list_entry(s, lv, list, it) : it;
+    const uint64_t* free_t = s.freem + (size_t)ea * s.MT;
+    const int2 pp = reinterpret_cast<const int2*>(s.pos)[ea];
+    const int px = pp.x, py = pp.y;
+    auto target = [&](int t, int& u, int& v) {  // as dist_kernel_t (extended coordinates)
+      if (t >= 5) {
+        const int r = (t - 5) / E, c = (t - 5) - r * E;
+        u = px + pad - s.ego + r;
+        v = py + pad - s.ego + c;
+      } else {
+        u = px + (t == 1 ? 1 : (t == 3 ? -1 : 0));
+        v = py + (t == 2 ? 1 : (t == 4 ? -1 : 0));
+      }
+    };
+    for (int t = tid; t < T; t += kBigThreads) s_d[t] = -1;
+    if (tid == 0) {
+      s_key = 0;
+      s_cov = 0;
+    }
+    for (int X = tid; X < s.Wp; X += kBigThreads) nxt[RWm * s.Wp + X] = 0xFFFF;
+    // ---- nxt, right to left over the word columns
+    int any = 0;
+    for (int q = RWm - 1; q >= 0; --q) {
+      __syncthreads();  // the last round's wc reads are done
+      big_stage_word(s, free_t, q, wc);
+      __syncthreads();
+      for (int X = tid; X < s.Wp; X += kBigThreads) {
+        const uint64_t w = wc[X];
+        any |= w != 0;
+        nxt[q * s.Wp + X] = w ? (uint16_t)(64 * q + __ffsll((unsigned long long)w) - 1) : nxt[(q + 1) * s.Wp + X];
+      }
+    }
+    if (any) s_cov = 1;
+    __syncthreads();
+    const bool cov = s_cov != 0;
+    // ---- the strips, left to right: wc holds word columns q0, q0 + 1 (slot q & 1)
+    int lastL[2] = {-kInf, -kInf};  // last covered extended column left of the strip, rows tid, tid + 1024
+    const int chunk = tid & (kBigCh - 1), pair = tid / kBigCh;
+    const int u0c = chunk * kBigCL;
+    const int nin = max(min(RX - u0c, kBigCL), 0);
+    const uint32_t rowmask = nin >= 32 ? ~0u : ((1u << nin) - 1u);
+    uint32_t bestkey = 0;
+    int bestv = -1;
+    const int tu_lo = min(px - 1, px + pad - s.ego), tu_hi = max(px + 1, px + pad + s.ego);
+    const int tv_lo = min(py - 1, py + pad - s.ego), tv_hi = max(py + 1, py + pad + s.ego);
+    int qs = -2;  // word columns in wc: qs, qs + 1
+    for (int st = 0; st < (cov ? nst : 0); ++st) {
+      const int c0 = st * kStrip, m0 = c0 - pad;  // extended / map column of the strip's first cell
+      const int q0 = m0 >= 0 ? m0 >> 6 : -1;
+      if (q0 != qs) {  // advance by one word column (or load both at the start)
+        __syncthreads();  // every read of the slot being replaced is done
+        if (q0 == qs + 1) {
+          big_stage_word(s, free_t, q0 + 1, wc + (size_t)((q0 + 1) & 1) * s.Wp);
+        } else {
+          big_stage_word(s, free_t, q0, wc + (size_t)(q0 & 1) * s.Wp);
+          big_stage_word(s, free_t, q0 + 1, wc + (size_t)((q0 + 1) & 1) * s.Wp);
+        }
+        qs = q0;
+        __syncthreads();
+      }
+      const int off = m0 - 64 * q0;  // 0..63
+      // ---- row pass: g of the strip's 32 cells of each row, 16 u16 pairs
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int u = tid + h * kBigThreads;
+        if (u >= kBigCh * kBigCL) continue;
+        uint2* grow = reinterpret_cast<uint2*>(G + u * kBigSP);
+        const int X = u - pad;
+        if (u >= RX || X < 0 || X >= s.Wp) {  // padding rows / the pad ring: no covered cell
+#pragma unroll
+          for (int k = 0; k < 8; ++k) grow[k] = make_uint2(~0u, ~0u);
+          continue;
+        }
+        const uint64_t wlo = q0 >= 0 ? wc[(size_t)(q0 & 1) * s.Wp + X] : 0ull;
+        const uint64_t whi = wc[(size_t)((q0 + 1) & 1) * s.Wp + X];
+        const uint32_t sb = (uint32_t)(off ? ((wlo >> off) | (whi << (64 - off))) : wlo);
+        // first covered extended column right of the strip (map column m0 + 32 on)
+        int firstR = kInf;
+        {
+          const int p = m0 + 32, qp = p >> 6;  // p >= 0 (pad < 32)
+          const uint64_t w = (qp == q0 ? wlo : whi) >> (p & 63);
+          if (w) {
+            firstR = p + __ffsll((unsigned long long)w) - 1 + pad;
+          } else {
+            const int nx = qp + 1 <= RWm ? nxt[(qp + 1) * s.Wp + X] : 0xFFFF;
+            if (nx != 0xFFFF) firstR = nx + pad;
+          }
+        }
+        const int lc = lastL[h];
+        if (sb == 0u) {
+          const uint32_t A = (uint32_t)min(c0 - lc, 0xFFFF - kStrip);
+          const uint32_t Bd = (uint32_t)min(firstR - c0, 0xFFFF);
+          const u16x2 Ap = {(uint16_t)A, (uint16_t)A}, Bp = {(uint16_t)Bd, (uint16_t)Bd};
+#pragma unroll
+          for (int k = 0; k < kStrip / 4; ++k) {
+            const u16x2 c0j = {(uint16_t)(4 * k), (uint16_t)(4 * k + 1)};
+            const u16x2 c1j = {(uint16_t)(4 * k + 2), (uint16_t)(4 * k + 3)};
+            const u16x2 g0 = __builtin_elementwise_min(Ap + c0j, Bp - c0j);
+            const u16x2 g1 = __builtin_elementwise_min(Ap + c1j, Bp - c1j);
+            grow[k] = make_uint2(__builtin_bit_cast(uint32_t, g0), __builtin_bit_cast(uint32_t, g1));
+          }
+        } else if (sb == ~0u) {
+#pragma unroll
+          for (int k = 0; k < kStrip / 4; ++k) grow[k] = make_uint2(0u, 0u);
+          lastL[h] = c0 + 31;
+        } else {
+#pragma unroll
+          for (int j4 = 0; j4 < kStrip; j4 += 4) {
+            uint32_t pq[2];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const int j = j4 + 2 * h2;
+              int gg[2];
+#pragma unroll
+              for (int k = 0; k < 2; ++k) {
+                const uint32_t le = sb & (0xFFFFFFFFu >> (31 - (j + k)));
+                const uint32_t ge = sb & (0xFFFFFFFFu << (j + k));
+                const int left = le ? c0 + 31 - __clz(le) : lc;
+                const int right = ge ? c0 + __ffs(ge) - 1 : firstR;
+                gg[k] = min(min(c0 + j + k - left, right - (c0 + j + k)), 0xFFFF);
+              }
+              pq[h2] = (uint32_t)gg[0] | ((uint32_t)gg[1] << 16);
+            }
+            grow[j4 >> 2] = make_uint2(pq[0], pq[1]);
+          }
+          lastL[h] = c0 + 31 - __clz(sb);
+        }
+      }
+      __syncthreads();
+      // ---- column pass (as dist_kernel_t's, 64 chunks of a column pair per wave)
+      int u0 = u0c;
+      asm volatile("" : "+v"(u0));
+      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(G) + u0 * (kBigSP / 2) + pair;
+      u16x2 tp[kBigCL], sd[kBigCL];
+      u16x2 pm = kNone2, sm = kNone2;
+#pragma unroll
+      for (int i = 0; i < kBigCL; ++i) {
+        const u16x2 g = __builtin_bit_cast(u16x2, g32[i * (kBigSP / 2)]);
+        const u16x2 uu = splat2(u0 + i);
+        tp[i] = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(g, kRowOff2), uu);
+        sd[i] = __builtin_elementwise_add_sat(g, uu);
+        pm = __builtin_elementwise_min(pm, tp[i]);
+        sm = __builtin_elementwise_min(sm, sd[i]);
+      }
+      __syncthreads();  // every G read of the strip is done: the next row pass may write
+      u16x2 run = excl_prefix_min64(pm), sfx = excl_suffix_min64(sm);
+#pragma unroll
+      for (int i = kBigCL - 1; i >= 0; --i) {
+        sfx = __builtin_elementwise_min(sfx, sd[i]);
+        sd[i] = __builtin_elementwise_sub_sat(sfx, splat2(u0 + i));
+      }
+      uint32_t klo = 0, khi = 0;
+#pragma unroll
+      for (int i = 0; i < kBigCL; ++i) {
+        const u16x2 uu = splat2(u0 + i);
+        run = __builtin_elementwise_min(run, tp[i]);
+        const u16x2 up = __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(run, uu), kRowOff2);
+        const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(up, sd[i])) &
+                           (uint32_t)__builtin_amdgcn_sbfe((int)rowmask, i, 1);
+        tp[i] = __builtin_bit_cast(u16x2, d);
+        klo = max(klo, (d << 16) | (uint32_t)(u0 + i));
+        khi = max(khi, (d & 0xFFFF0000u) | (uint32_t)(u0 + i));
+      }
+      const int v = c0 + 2 * pair;
+      if (v < RY && klo > bestkey) {
+        bestkey = klo;
+        bestv = v;
+      }
+      if (v + 1 < RY && khi > bestkey) {
+        bestkey = khi;
+        bestv = v + 1;
+      }
+      const bool keep = v + 1 >= tv_lo && v <= tv_hi && u0 + kBigCL > tu_lo && u0 <= tu_hi;
+      if (keep) {
+        for (int t = 0; t < T; ++t) {
+          int tu, tv;
+          target(t, tu, tv);
+          if ((tv == v || tv == v + 1) && tu >= u0 && tu < u0 + kBigCL && tu < RX) {
+            uint32_t val = 0;
+#pragma unroll
+            for (int i = 0; i < kBigCL; ++i) val = (u0 + i == tu) ? __builtin_bit_cast(uint32_t, tp[i]) : val;
+            s_d[t] = (int)(tv == v ? (val & 0xFFFFu) : (val >> 16));
+          }
+        }
+      }
+    }
+    const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
+    if (cov && vmax >= 0) {
+      const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
+      const int far = abs(ubest - (px + pad)) + abs(vbest - (py + pad));
+      atomicMax(&s_key, ((unsigned long long)vmax << 48) | ((unsigned long long)far << 32) |
+                            ((unsigned long long)ubest << 16) | (unsigned long long)vbest);
+    }
+    __syncthreads();
+    const int M = cov ? (int)(s_key >> 48) : -1;
+    const float Mf = (float)M;
+    if (tid == 0) {
+      const int wu = (int)((s_key >> 16) & 0xFFFF), wv = (int)(s_key & 0xFFFF);
+      reinterpret_cast<int2*>(s.dist_mw)[ea] = make_int2(M, pack_witness(wu - pad, wv - pad));
+    }
+    if (post) {
+      float* dst = dist_obs + (size_t)ea * E * E;
+      for (int t = 5 + tid; t < T; t += kBigThreads) dst[t - 5] = dist_value((float)(cov ? s_d[t] : -1), Mf);
+    }
+    float* pd = pre_out + (size_t)ea * 8;
+    if (tid == 0) pd[0] = Mf;
+    if (tid < 5) pd[1 + tid] = (float)(cov ? s_d[tid] : -1);
+    __syncthreads();  // the LDS is reused by the next item
+  }
+  // the work list's bookkeeping, as dist_kernel_t's (mode 0 with a list)
+  if (list && threadIdx.x == 0) {
+    uint32_t* cnt = count;
+    if (n_items == 0) {
+      if (blockIdx.x == 0) {
+        cnt[2] = cnt[4] = 0;
+        if (s.dist_tot) s.dist_tot[3] += 1ull;
+      }
+    } else {
+      __threadfence();
+      if (atomicAdd(cnt + 1, 1u) == gridDim.x - 1) {
+        uint32_t nl = 0;
+        for (int k = 0; k < kListShards; ++k) nl += atomicExch(s.dist_shc + k * kShardStride, 0u);
+        const uint32_t nh = atomicExch(cnt + 3, 0u);
+        atomicExch(cnt + 2, nl);
+        atomicExch(cnt + 4, nh);
+        atomicExch(cnt + 1, 0u);
+        if (s.dist_tot) {
+          s.dist_tot[0] += nl;
+          s.dist_tot[1] += nh;
+          s.dist_tot[2] += nl - nh;
+          s.dist_tot[3] += 1ull;
+        }
+      }
+    }
+  }
+}
+
+static hipError_t launch_big(const State& s, int pad, int post, float* pre_out, float* dist_obs,
+                             const uint32_t* list, uint32_t* count, unsigned grid, hipStream_t stream) {
+  const size_t lds = big_lds(s.Wp, s.TC, 5 + s.E * s.E).total;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dist_big_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  // a list: one resident workgroup per CU strides over it (LDS: one per CU)
+  const unsigned g = list ? (grid < 256u ? grid : 256u) : grid;
+  hipLaunchKernelGGL(dist_big_kernel, dim3(g), dim3(kBigThreads), lds, stream, s, pad, post, pre_out, dist_obs, list,
+                     count);
+  return hipGetLastError();
+}
+
+size_t dist_lds_bytes(const State& s, int pad) {
+  if (s.Wp + 2 * pad > kMaxRows) return big_lds(s.Wp, s.TC, 5 + s.E * s.E).total;
+  return dt_lds(s.Wp + 2 * pad, s.Lp + 2 * pad, s.MT, 5 + s.E * s.E).total;
+}
+
+// extended rows the distance transform takes (dist_big_kernel past
+// kMaxRows) / that the LDS-bitboard transform, its split parts and the
+// top-cell cache take
+int dist_max_rows() { return kBigMaxRows; }
+int dist_cache_max_rows() { return kMaxRows; }
 
 hipError_t launch_dist(const State& s, int pad, int post, float* pre_out, float* dist_obs,
                        hipStream_t stream) {

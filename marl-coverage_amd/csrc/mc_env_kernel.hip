@@ -2276,7 +2276,10 @@ static void launch_one(const State& s, int mode, const uint8_t* actions, const u
 using Dynamic = Shape<0, 0, 0, 0, 0>;
 using ShapeC2 = Shape<4, 10, 21, 2, 10, 8>;      // the bench workload
 using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs layers)
-using ShapeC4 = Shape<8, 20, 360, 2, 20, 15>;    // 360 beams, R=20
+// 360 beams, R=20; its fan: 64 sector slots, 2 special
+// beams, 1,024 LUT words + 32 pair records x 42 + 2 x 8 = 2,384 words
+using ShapeC4 = Shape<8, 20, 360, 2, 20, 15, 3, 0, 64, 2, 2384>;
+using ShapeC4R = Shape<8, 20, 360, 2, 20, 15>;  // the same without a baked fan (the ray march: MARLCOV_FAN=0)
 using ShapeC5 = Shape<16, 10, 21, 2, 10, 8, 4, 1>;  // 16 agents, egoradius 2, dist_reward (4 obs layers)
 
 #define MC_EL(T, P, W, SH, NAME) \
@@ -2310,6 +2313,7 @@ EnvLaunch select_env(const State& s, int nt, int epw) {
     }
   }
   if (nt == 256 && fits32 && spec && ShapeC4::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4, "u64,C4");
+  if (nt == 256 && fits32 && spec && ShapeC4R::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4R, "u64,C4");
   switch (nt) {
     case 64: return MC_EL(64, 1, uint64_t, Dynamic, "u64,generic");
     case 128: return MC_EL(128, 1, uint64_t, Dynamic, "u64,generic");

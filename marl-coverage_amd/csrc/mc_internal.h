@@ -277,16 +277,22 @@ __host__ __device__ inline size_t slot_stride(size_t slot_lds) {
 // LC: obs layers of an EGO shape (3; 4 with dijkstra_input, whose layer 3 the
 // dijkstra kernel writes after the env kernel, or with dist_reward, whose
 // layer 3 is the float buffer: 0 in the uint8 obs).  DS: an EGO shape's
-// dist_reward flag (baked in).
-template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3, int DS_ = 0>
+// dist_reward flag (baked in).  FN / FS / FW: a dense-beam shape's fan
+// march -- sector slots, special beams and fan words (mc_set_beam_table's
+// build_fan; its trip count is KM): the fan's LDS offsets (carve) then fold
+// to constants instead of living in SGPRs across the kernel.
+template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3, int DS_ = 0, int FN_ = 0,
+          int FS_ = 0, int FW_ = 0>
 struct Shape {
   static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_, LC = LC_, DS = DS_;
+  static constexpr int FN = FN_, FS = FS_, FW = FW_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
            (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
            (EGO_ == 0 || (s.ego == EGO_ && s.Lc == LC_ && (s.dist != 0) == (DS_ != 0))) &&
            (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_)) &&
-           (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_));
+           (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_)) &&
+           (FN_ == 0 || (s.fan_nsec == FN_ && s.fan_nspec == FS_ && s.fan_words == FW_ && s.fan_kt == KM_));
   }
 };
 
@@ -317,8 +323,16 @@ __device__ __forceinline__ void specialize(State& s) {
     s.mg_LcE = magic_div(SH::LC * (2 * SH::EGO + 1));
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
+  if constexpr (SH::FN > 0) {
+    s.fan_nsec = SH::FN;
+    s.fan_nspec = SH::FS;
+    s.fan_words = SH::FW;
+    s.fan_kt = SH::KM;
+  }
   if constexpr (SH::KN > 0) s.beam_kmin = SH::KN;
   if constexpr (SH::EGO > 0) s.dist = SH::DS;  // an EGO shape bakes in its dist_reward flag
+  // (LC 3 / 4 leaves no room for minimap layers: mini_map_rad = 0, pad = ego)
+  if constexpr (SH::EGO > 0 && SH::LC <= 4) s.pad = SH::EGO;
 }
 
 }  // namespace mc

@@ -7,8 +7,10 @@ tests/golden/maps; SURVEY 8(f) rank 4, gridmaker.py:82-102).
   with observation, reward and done equal every step.
 * A bg2_1073x1073 map (the grid-size scaling axis) stepped in a
   batch against the oracle, at the C2 and C4 sensor configs.
-* dist_reward on that map is rejected by mc_create with a message (the
-  transform's 832-row limit).
+* dist_reward on that map (1,079 extended rows: the big-map distance
+  kernel, mc_dist.hip dist_big_kernel) against the oracle, (M, witness) of
+  every map checked against a fresh transform; a grid past the big kernel's
+  1,088 rows is rejected by mc_create with a message.
 """
 import os
 
@@ -74,12 +76,31 @@ def test_bg2_1073_batch_matches_oracle(torch_cuda, shape):
     assert resets >= B
 
 
-def test_bg2_1073_dist_reward_is_rejected(torch_cuda):
-    """dist_reward on a 1073x1073 map: 1,079 extended rows exceed the distance
-    transform's 832 (mc_build_param(MC_PARAM_DIST_MAX_ROWS)); mc_create
-    fails with that message instead of running a wrong transform."""
+def test_bg2_1073_dist_reward_matches_oracle(torch_cuda):
+    """dist_reward (the C5 frontier reward) on the 1073x1073 reference map:
+    1,079 extended rows, past the LDS-bitboard transform's 832, so every
+    listed map runs the big-map kernel (no top-cell cache).  Two envs x 4
+    agents tracked by the oracle from the reset through 16 steps with an
+    auto-reset (maxsteps 8): reward with the float32 distance terms, the
+    float distance obs layer, maps, and every known (M, witness) against a
+    fresh transform (dec_grid_rl.py:222-223,239-240,260-282)."""
     import marlcov
     from marlcov import _lib
-    assert _lib.load().mc_build_param(_lib.PARAM_DIST_MAX_ROWS) == 832
+    torch = torch_cuda
+    assert _lib.load().mc_build_param(_lib.PARAM_DIST_MAX_ROWS) == 1088
+    cfg = base_cfg(numrobot=4, dist_reward=1, maxsteps=8)
+    env = marlcov.BatchCoverageEnv(cfg, 2, grids=[big_map()], auto_reset=True, seed=5)
+    env.reset()
+    resets = run_against_oracle(torch, env, cfg, np.random.RandomState(79), 16, [0, 1], 5, "bg2_1073 dist",
+                                dist_check=True, sentinel_p=0.0)
+    assert resets >= 2
+
+
+def test_dist_reward_rows_past_the_big_kernel_are_rejected(torch_cuda):
+    """Extended grids past the big-map kernel's 1,088 rows: mc_create fails
+    with a message instead of running a wrong transform."""
+    import marlcov
+    from marlcov import _lib
+    g = np.ones((1090, 40))
     with pytest.raises(_lib.MarlcovError, match="extended rows exceed"):
-        marlcov.BatchCoverageEnv(base_cfg(numrobot=4, dist_reward=1), 2, grids=[big_map()], seed=1)
+        marlcov.BatchCoverageEnv(base_cfg(numrobot=2, dist_reward=1), 1, grids=[g], seed=1)

@@ -55,9 +55,9 @@ def test_build_params(lib):
     from marlcov import _lib
     assert lib.mc_build_param(_lib.PARAM_DIST_CACHE_CELLS) == 512
     assert lib.mc_build_param(_lib.PARAM_DIST_T) == 20
-    # the transform's row limit (bg2_1073x1073 maps, 1,079
-    # extended rows at egoradius 2, are rejected with dist_reward)
-    assert lib.mc_build_param(_lib.PARAM_DIST_MAX_ROWS) == 832
+    # the distance transform's row limit: the big-map kernel past the LDS
+    # bitboard's 832 rows (bg2_1073x1073: 1,079 extended rows at egoradius 2)
+    assert lib.mc_build_param(_lib.PARAM_DIST_MAX_ROWS) == 1088
     assert lib.mc_build_param(99) == -1
 
 

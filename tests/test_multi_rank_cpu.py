@@ -162,7 +162,8 @@ def _bench(args, env_extra=None, timeout=240):
     env.update(env_extra or {})
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, cwd=ROOT,
                        capture_output=True, text=True, timeout=timeout)
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert all(ln.startswith("{") for ln in lines), p.stdout  # stdout carries the JSON line only
     return p.returncode, [json.loads(ln) for ln in lines], p.stderr
 
 
