@@ -939,7 +939,9 @@ __device__ __forceinline__ void fan_pair(const State& s, const Lds<WT>& L, const
     for (int u = 0; u < SU; ++u) {
       A0 &= e0[u] >> 16;  // in range (a step past the trip count, or an empty sector, has e = 0)
       A1 &= e1[u] >> 16;
-      const uint32_t l0 = spread[(e0[u] & 0x7C0u) | A0], l1 = spread[(e1[u] & 0x7C0u) | A1];
+      // (+ for |: the fields are disjoint, A <= 63 -- one v_add3 with the
+      // LUT base instead of an OR and an add)
+      const uint32_t l0 = spread[(e0[u] & 0x7C0u) + A0], l1 = spread[(e1[u] & 0x7C0u) + A1];
       A0 &= ~k0v[u];
       A1 &= ~k1v[u];
       F0[u] = l0 & ~S0[u];  // new marks (the cells the agent has not seen)
@@ -2280,7 +2282,17 @@ using ShapeC2D = Shape<4, 10, 21, 2, 10, 8, 4>;  // C2 + dijkstra_input (4 obs l
 // beams, 1,024 LUT words + 32 pair records x 42 + 2 x 8 = 2,384 words
 using ShapeC4 = Shape<8, 20, 360, 2, 20, 15, 3, 0, 64, 2, 2384>;
 using ShapeC4R = Shape<8, 20, 360, 2, 20, 15>;  // the same without a baked fan (the ray march: MARLCOV_FAN=0)
+// the bench instantiations (bench.py CONFIGS: 256x256 / 128x128 / 512x512
+// grids, auto-reset, no comm graph); other grids run the shapes above
+using ShapeC4B = Shape<8, 20, 360, 2, 20, 15, 3, 0, 64, 2, 2384, 258>;
+using ShapeC2B = Shape<4, 10, 21, 2, 10, 8, 3, 0, 0, 0, 0, 130>;
+using ShapeC5B = Shape<16, 10, 21, 2, 10, 8, 4, 1, 0, 0, 0, 514>;
 using ShapeC5 = Shape<16, 10, 21, 2, 10, 8, 4, 1>;  // 16 agents, egoradius 2, dist_reward (4 obs layers)
+
+#ifndef MC_BENCH_SHAPES  // build knob (A/B): 0 leaves the grid-baked bench instantiations out
+#define MC_BENCH_SHAPES 1
+#endif
+constexpr bool kBenchShapes = MC_BENCH_SHAPES != 0;
 
 #define MC_EL(T, P, W, SH, NAME) \
   EnvLaunch { "env_kernel<" #T "," #P "," NAME ">", &launch_one<T, P, W, SH> }
@@ -2295,6 +2307,7 @@ EnvLaunch select_env(const State& s, int nt, int epw) {
   const bool fits32 = (uint64_t)s.B * s.N * mtb < (1ull << 32) && (uint64_t)s.G * mtb < (1ull << 32);
   const bool spec = getenv_spec();
   if (epw == 2) {
+    if (narrow && fits32 && spec && kBenchShapes && ShapeC2B::matches(s)) return MC_EL(64, 2, uint32_t, ShapeC2B, "u32,C2");
     if (narrow && fits32 && spec && ShapeC2::matches(s)) return MC_EL(64, 2, uint32_t, ShapeC2, "u32,C2");
     if (narrow && fits32 && spec && ShapeC2D::matches(s)) return MC_EL(64, 2, uint32_t, ShapeC2D, "u32,C2D");
     if (narrow) return MC_EL(64, 2, uint32_t, Dynamic, "u32,generic");
@@ -2303,6 +2316,7 @@ EnvLaunch select_env(const State& s, int nt, int epw) {
   if (narrow) {
     if (nt == 64 && fits32 && spec && ShapeC2::matches(s)) return MC_EL(64, 1, uint32_t, ShapeC2, "u32,C2");
     if (nt == 64 && fits32 && spec && ShapeC2D::matches(s)) return MC_EL(64, 1, uint32_t, ShapeC2D, "u32,C2D");
+    if (nt == 128 && spec && kBenchShapes && ShapeC5B::matches(s)) return MC_EL(128, 1, uint32_t, ShapeC5B, "u32,C5");
     if (nt == 128 && spec && ShapeC5::matches(s)) return MC_EL(128, 1, uint32_t, ShapeC5, "u32,C5");
     switch (nt) {
       case 64: return MC_EL(64, 1, uint32_t, Dynamic, "u32,generic");
@@ -2312,6 +2326,7 @@ EnvLaunch select_env(const State& s, int nt, int epw) {
       default: return MC_EL(1024, 1, uint32_t, Dynamic, "u32,generic");
     }
   }
+  if (nt == 256 && fits32 && spec && kBenchShapes && ShapeC4B::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4B, "u64,C4");
   if (nt == 256 && fits32 && spec && ShapeC4::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4, "u64,C4");
   if (nt == 256 && fits32 && spec && ShapeC4R::matches(s)) return MC_EL(256, 1, uint64_t, ShapeC4R, "u64,C4");
   switch (nt) {

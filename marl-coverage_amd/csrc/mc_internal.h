@@ -280,19 +280,23 @@ __host__ __device__ inline size_t slot_stride(size_t slot_lds) {
 // dist_reward flag (baked in).  FN / FS / FW: a dense-beam shape's fan
 // march -- sector slots, special beams and fan words (mc_set_beam_table's
 // build_fan; its trip count is KM): the fan's LDS offsets (carve) then fold
-// to constants instead of living in SGPRs across the kernel.
+// to constants instead of living in SGPRs across the kernel.  BW: a bench
+// instantiation -- square padded grids of side BW (the tile geometry and the
+// beam-bit row length fold to constants) with the bench's episode flags (no
+// comm graph, grids kept on reset, auto-reset on).
 template <int N_, int H_, int NB_, int EGO_, int KM_, int KN_ = 0, int LC_ = 3, int DS_ = 0, int FN_ = 0,
-          int FS_ = 0, int FW_ = 0>
+          int FS_ = 0, int FW_ = 0, int BW_ = 0>
 struct Shape {
   static constexpr int N = N_, H = H_, NB = NB_, EGO = EGO_, KM = KM_, KN = KN_, LC = LC_, DS = DS_;
-  static constexpr int FN = FN_, FS = FS_, FW = FW_;
+  static constexpr int FN = FN_, FS = FS_, FW = FW_, BW = BW_;
   __host__ __device__ static bool matches(const State& s) {
     return (N_ == 0 || s.N == N_) && (H_ == 0 || s.H == H_) &&
            (NB_ == 0 || (s.sensor == 0 && s.nbeams == NB_)) &&
            (EGO_ == 0 || (s.ego == EGO_ && s.Lc == LC_ && (s.dist != 0) == (DS_ != 0))) &&
            (KM_ == 0 || (s.sensor == 0 && s.beam_kmax == KM_)) &&
            (KN_ == 0 || (s.sensor == 0 && s.beam_kmin == KN_)) &&
-           (FN_ == 0 || (s.fan_nsec == FN_ && s.fan_nspec == FS_ && s.fan_words == FW_ && s.fan_kt == KM_));
+           (FN_ == 0 || (s.fan_nsec == FN_ && s.fan_nspec == FS_ && s.fan_words == FW_ && s.fan_kt == KM_)) &&
+           (BW_ == 0 || (s.Wp == BW_ && s.Lp == BW_ && s.comm_r == 0 && s.grid_mode == 0 && s.auto_reset == 1));
   }
 };
 
@@ -323,6 +327,17 @@ __device__ __forceinline__ void specialize(State& s) {
     s.mg_LcE = magic_div(SH::LC * (2 * SH::EGO + 1));
   }
   if constexpr (SH::KM > 0) s.beam_kmax = SH::KM;
+  if constexpr (SH::BW > 0) {  // (mc_capi.hip mc_create / mc_set_beam_table derive the same)
+    constexpr int T8 = (SH::BW + 7) / 8, T32 = (T8 + 3) / 4;
+    s.Wp = s.Lp = SH::BW;
+    s.TR = s.TC = T8;
+    s.TRS = s.TCS = T32;
+    s.MT = T32 * T32 * 16;
+    s.bcmax = SH::BW;
+    s.comm_r = 0;
+    s.grid_mode = 0;
+    s.auto_reset = 1;
+  }
   if constexpr (SH::FN > 0) {
     s.fan_nsec = SH::FN;
     s.fan_nspec = SH::FS;
