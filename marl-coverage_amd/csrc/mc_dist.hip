@@ -583,6 +583,18 @@ constexpr bool kBalance = MC_DIST_BALANCE != 0;
 #ifndef MC_DIST_ACQREL  // build knob (A/B): 0 = round 5's relaxed arrival add (ordering by vmcnt + sc1 only)
 #define MC_DIST_ACQREL 1
 #endif
+#ifndef MC_DIST_HO_SC1  // build knob (A/B): 0 = plain stores / loads for the hand-off (the acq_rel arrival orders them)
+#define MC_DIST_HO_SC1 1
+#endif
+#ifndef MC_DIST_SKIP_IDLE  // build knob (A/B): 1 = idle parts skip staging (measured slower, round 6)
+#define MC_DIST_SKIP_IDLE 0
+#endif
+// A part that the balanced split gives no running strip (fewer running
+// strips than parts) stages nothing: it only arrives, and stages the map
+// after all if it is the merger and the cache pass has to run.  Measured
+// slower (C5 steady 142.5 vs 140.3 us, default window 153.7 vs 151.6 us,
+// profiles/r6/hoab/): off
+constexpr bool kSkipIdle = MC_DIST_SKIP_IDLE != 0;
 #ifndef MC_DIST_PARTLIST  // build knob (A/B): 1 = part lists (below); off: measured slower, round 6
 #define MC_DIST_PARTLIST 0
 #endif
@@ -599,6 +611,10 @@ constexpr bool kBalance = MC_DIST_BALANCE != 0;
 // parity-tested (tests/test_gpu_shapes.py, 8 envs: the mass reset splits
 // every map with theta0 = 0).
 constexpr bool kPartList = MC_DIST_PARTLIST != 0 && kOnePass;
+// the split parts' hand-off words as agent-scope relaxed atomics (`sc1`),
+// or, under the acq_rel arrival, plain stores and loads (no faster within
+// the noise, profiles/r6/hoab/: kept sc1)
+constexpr bool kHoSc1 = MC_DIST_HO_SC1 != 0 || MC_DIST_ACQREL == 0;
 
 // The strips a full transform of map ea runs with the lower bound theta of
 // its new max(d) (bit st; the rest are pruned, dist_kernel_t's strip loop):
@@ -714,6 +730,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     // splitting the map's running strips evenly (strip_run_mask; without a
     // mask, its strips)
     int st_lo = part * nstrips_all / S, st_hi = (part + 1) * nstrips_all / S;
+    bool idle = false;  // no running strip in this part's range (kSkipIdle)
     if (kBalance && mode == 2 && S > 1 && s.dist_rmask) {
       const uint64_t rm = s.dist_rmask[ea];
       if (rm) {
@@ -729,6 +746,9 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         };
         st_lo = bound(part);
         st_hi = bound(part + 1);
+        const uint64_t upto_hi = st_hi >= 64 ? ~0ull : low_mask(st_hi);
+        const uint64_t upto_lo = st_lo >= 64 ? ~0ull : low_mask(st_lo);
+        idle = kSkipIdle && (rm & upto_hi & ~upto_lo) == 0ull;
       }
     }
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, dflags = 0, tsa = 0, tsb = 0;
@@ -843,9 +863,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       merge_parts(false);
       need_cb = s_cov && !(((kOnePass && theta0 > 0) || kPartList) && s_ccount <= kDistK);  // the second pass
     }
-    if (!fast && need_cb) {
-      if (mode != 3)  // (mode 3 holds the parts' targets)
-        for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
+    // the map's row bitboard (Cb) in LDS
+    auto stage_cb = [&]() {
       {
         // the agent's tiles as map rows in the strip area (free until the
         // strips start): a thread takes 8 tiles of one tile row (one 64-column
@@ -936,8 +955,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
         if (any) s_cov = 1;
       }
       __syncthreads();
+    };
+    if (!fast && need_cb && !idle) {
+      if (mode != 3)  // (mode 3 holds the parts' targets)
+        for (int t = tid; t < T; t += kDtThreads) s_d[t] = -1;
+      stage_cb();
     }
-    const bool cov = fast || s_cov != 0;
+    bool cov = fast || s_cov != 0;
     DSTAMP(ts1);
 
     // row-pass registers: a thread owns rows tid and tid + kDtThreads
@@ -1219,11 +1243,11 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (tid == 0 && s_key) atomicMax(s.dist_gkey + ea, s_key);
       for (int t = tid; t < T; t += kDtThreads)
         if (s_d[t] >= 0) {
-          if (t < 5) st_ho(pre_out + (size_t)ea * 8 + 1 + t, (float)s_d[t], kFused);
-          else st_ho(dist_obs + (size_t)ea * E * E + (t - 5), (float)s_d[t], kFused);
+          if (t < 5) st_ho(pre_out + (size_t)ea * 8 + 1 + t, (float)s_d[t], kFused && kHoSc1);
+          else st_ho(dist_obs + (size_t)ea * E * E + (t - 5), (float)s_d[t], kFused && kHoSc1);
         }
       for (int st = st_lo + tid; st < min(st_hi, kMaxTrack); st += kDtThreads)
-        if ((ran >> st) & 1ull) st_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, (uint32_t)min(s_smax[st], 0xFFFF), kFused);
+        if ((ran >> st) & 1ull) st_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, (uint32_t)min(s_smax[st], 0xFFFF), kFused && kHoSc1);
       bool part_list = false;  // this part collected its own candidates (theta0 = 0)
       if (kPartList && theta0 == 0 && s.dist_ch) {
         // the part's own maximum and the best key the parts published so far
@@ -1262,7 +1286,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           if (n <= kDistK)
             for (int k = tid; k < n; k += kDtThreads)
               if (base + k < (uint32_t)kGCand)
-                st_ho(s.dist_gcand + (size_t)fi * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused);
+                st_ho(s.dist_gcand + (size_t)fi * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused && kHoSc1);
         }
       }
       if constexpr (kFused) {
@@ -1285,7 +1309,8 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (merged) {
         // the map's bitboard is staged here (every part stages it): a second
         // cache pass, if the parts' lists overflowed, needs no restaging
-        merge_parts(true);
+        merge_parts(kHoSc1);
+        cov = s_cov != 0;  // the map's, from the parts' keys (an idle merger staged nothing)
       }
 #ifdef MC_DIST_STAMPS
       {  // a part (flag bit 52): stage, strips, publish (mode 3 leaves these)
@@ -1352,6 +1377,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
           cnt = s_kept;
           dflags |= 1ull << 49;
         } else if (cov && M >= 0) {
+          if (idle) stage_cb();  // an idle part merging: the bitboard for the pass
           dflags |= 1ull << 50;
           __syncthreads();  // every thread has read s_ccount
           if (tid == 0) s_ccount = 0;
