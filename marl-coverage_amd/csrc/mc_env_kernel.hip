@@ -1453,18 +1453,80 @@ __device__ __forceinline__ void store_tiles(const State& s, const Ctx<NT, EPW, W
   }
 }
 
-// sense -> (lidar: gather) -> (single tool) -> merge, with the barriers
-template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0, int RPLX = 0>
-__device__ __forceinline__ void sense_and_merge(const State& s, const Ctx<NT, EPW, WT>& C,
-                                                Items<KI>& I) {
+#ifndef MC_RELOAD  // build knob (A/B): 0 keeps one State for the whole kernel
+#define MC_RELOAD 1
+#endif
+// The kernel's State re-read at a phase boundary from the kernel arguments
+// through an opaque kernarg pointer: the fields the next phase uses are
+// loaded there (s_load, scalar cache) instead of staying live in SGPRs across
+// the whole kernel, where the C5 shape's ~35 pointers spilled to VGPR lanes
+// (v_writelane at entry, a VALU v_readlane at every use).  One env per
+// workgroup only: the two-env C2 wave spilled more with it and ran slower
+// (8.38 vs 8.22 us; C4 126.6 -> 123.3 us, C5 steady 140.7 -> 136.4 us per
+// step, profiles/r6/rlab/)
+// The env kernel's one argument: the State and the step's buffers
+struct EnvIO {
+  const uint8_t* actions;   // [B][N] (MODE_STEP)
+  const uint8_t* env_mask;  // [B] envs to reset (MODE_RESET; null: all)
+  const int32_t* inj_pos;   // [B][N][2] injected start cells (null: device draw)
+  double* reward_out;
+  uint8_t* done_out;
+  uint8_t* obs_out;
+  uint8_t* adj_out;  // null: no comm graph output
+  int mode;
+};
+struct EnvArgs {
+  State s;
+  EnvIO io;
+};
+template <class SH, int EPW>
+__device__ __forceinline__ void reload_state(State& s, EnvIO& io) {
+  if constexpr (MC_RELOAD != 0 && EPW == 1) {
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();  // the EnvArgs
+    asm volatile("" : "+s"(kp));
+    const EnvArgs& A = *(const EnvArgs*)kp;
+    s = A.s;
+    io = A.io;
+    specialize<SH>(s);
+  }
+}
+template <class SH, int EPW>
+__device__ __forceinline__ void reload_state(State& s) {
+  EnvIO io;
+  reload_state<SH, EPW>(s, io);
+}
+// (also inside sense_and_merge / reset_env: slower, C4 123.9 vs 123.2 us, C5
+// steady 137.0 vs 136.3 us, profiles/r6/rlab2/)
+#ifndef MC_RELOAD_INNER  // build knob (A/B): 1 = re-read inside sense_and_merge / reset_env too
+#define MC_RELOAD_INNER 0
+#endif
+template <class SH, int EPW>
+struct Reload {
+  __device__ __forceinline__ void operator()(State& s) const {
+    if constexpr (MC_RELOAD_INNER != 0) reload_state<SH, EPW>(s);
+  }
+};
+struct NoReload {
+  __device__ __forceinline__ void operator()(State&) const {}
+};
+
+// sense -> (lidar: gather) -> (single tool) -> merge, with the barriers (rl:
+// the State re-read between them, reload_state)
+template <int NT, int EPW, typename WT, int KI, int SUK, int NS, int KN, int KM = 0, int RPLX = 0,
+          class RL = NoReload>
+__device__ __forceinline__ void sense_and_merge(const State& s0, const Ctx<NT, EPW, WT>& C,
+                                                Items<KI>& I, RL rl = RL()) {
+  State s = s0;
   if (MC_ABL != 5) sense<NT, EPW, WT, SUK, KN, KM, RPLX>(s, C);
   __syncthreads();
   STAMP(13);
+  rl(s);
   if (s.sensor == 0) {
     gather_marks<NT, EPW, WT, KI>(s, C, I);
     __syncthreads();
   }
   STAMP(4);
+  rl(s);
   if (s.sst) {
     single_tool<NT, EPW, WT>(s, C);
     __syncthreads();
@@ -1486,9 +1548,10 @@ __device__ __forceinline__ void set_agent(const State& s, const Lds<WT>& L, int 
   L.by[a] = (y - s.H - 1) >> 3;
 }
 
-template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32, int KM = 0, int RPLX = 0>
+template <int NT, int EPW, typename WT, int SUK, int NS, int KN, bool O32, int KM = 0, int RPLX = 0,
+          class RL = NoReload>
 __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>& C,
-                                          const int32_t* inj_pos) {
+                                          const int32_t* inj_pos, RL rl = RL()) {
   constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
   constexpr int KI = Ctx<NT, EPW, WT>::KI;
   const Lds<WT>& L = C.L;
@@ -1563,7 +1626,7 @@ __device__ __forceinline__ void reset_env(const State& s, const Ctx<NT, EPW, WT>
   zero_marks<NT, EPW, WT>(s, C);
   stage<NT, EPW, WT, KI, O32>(s, C, g, /*load_masks=*/false, I);
   __syncthreads();
-  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN, KM, RPLX>(s, C, I);
+  sense_and_merge<NT, EPW, WT, KI, SUK, NS, KN, KM, RPLX>(s, C, I, rl);
   store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
   __syncthreads();
   if (C.sub == 0) {
@@ -1822,15 +1885,11 @@ constexpr int env_min_waves() {
 }
 
 template <int NT, int EPW, typename WT, class SH>
-__global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(State s_in, int mode, const uint8_t* __restrict__ actions,
-                                                 const uint8_t* __restrict__ env_mask,
-                                                 const int32_t* __restrict__ inj_pos,
-                                                 double* __restrict__ reward_out,
-                                                 uint8_t* __restrict__ done_out,
-                                                 uint8_t* __restrict__ obs_out,
-                                                 uint8_t* __restrict__ adj_out) {
-  State s = s_in;
+__global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvArgs args) {
+  State s = args.s;
   specialize<SH>(s);
+  EnvIO io = args.io;
+  const int mode = io.mode;
   using CtxT = Ctx<NT, EPW, WT>;
   constexpr int LPE = CtxT::LPE;
   constexpr int KI = CtxT::KI;
@@ -1882,9 +1941,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
   // holds all robots; other lanes of other builds read robot 0)
   const int ag = (FRONT && FrontQuad<NSM>::ok) ? (C.sub & (N - 1)) : (C.sub < N ? C.sub : 0);
   // absent inputs read a harmless valid byte instead (no branch, no wait)
-  const uint8_t* ab = is_step ? actions : reinterpret_cast<const uint8_t*>(s.pos);
+  const uint8_t* ab = is_step ? io.actions : reinterpret_cast<const uint8_t*>(s.pos);
   const uint32_t eN = (uint32_t)e * (uint32_t)N;
-  const uint8_t* mb = env_mask != nullptr ? env_mask + e : reinterpret_cast<const uint8_t*>(s.pos);
+  const uint8_t* mb = io.env_mask != nullptr ? io.env_mask + e : reinterpret_cast<const uint8_t*>(s.pos);
   const int2 p0 = el<O32>(reinterpret_cast<const int2*>(s.pos), eN + ag);
   const int act_raw = el<O32>(ab, is_step ? eN + ag : 0), act0_raw = el<O32>(ab, is_step ? eN : 0);
   const int req_raw = mb[0];
@@ -1924,7 +1983,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
                "v"(bm0.x), "v"(bm0.w), "v"(mwv.x), "v"(mwv.y), "v"(chd.x), "v"(chd.w), "v"(chb.y));
   const int act = is_step ? act_raw : 255;
   const int act0 = is_step ? act0_raw : 0;      // agent 0's byte: the sentinel
-  const int req = env_mask != nullptr ? req_raw : 1;
+  const int req = io.env_mask != nullptr ? req_raw : 1;
 
   const bool sentinel = valid && is_step && act0 == 255;
   const bool reset_req = valid && !is_step && req != 0;
@@ -1964,6 +2023,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     for (int b = C.sub + LPE; b < s.nbeams; b += LPE) L.beams[b] = s.beams[b];
   }
   __syncthreads();
+  reload_state<SH, EPW>(s, io);
 
   if (active) {
     STAMP(1);
@@ -2010,6 +2070,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     const int numfree = el<O32>(s.numfree, g0);
     __syncthreads();
     STAMP(2);
+    reload_state<SH, EPW>(s, io);
     // (the same loop on the scalar unit, robots read by v_readlane, was
     // slower: 10.17 vs 9.83 us at C2 -- +178 SALU for -17 VALU per wave)
     if constexpr (!FRONT && !EARLY) {  // (FRONT, EARLY: moved during round trip 2)
@@ -2029,6 +2090,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       __syncthreads();
     }
     STAMP(3);
+    reload_state<SH, EPW>(s, io);
     // dist_reward: lane i < N loads its agent's PRE terms (the last step's
     // dist kernels wrote them) now that its move is known; they land during
     // the sensing
@@ -2043,9 +2105,10 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       dpre0 = pr[0];
       dprek = pr[1 + k];
     }
-    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM, RPLK>(s, C, I);
+    sense_and_merge<NT, EPW, WT, KI, SUK, NSM, SH::KN, SH::KM, RPLK>(s, C, I, Reload<SH, EPW>());
     __syncthreads();
     STAMP(5);
+    reload_state<SH, EPW>(s, io);
     // every lane of the slot computes the reward and done (the same values:
     // no broadcast round trip or barrier before the stores); lane 0 stores
     bool do_reset;
@@ -2093,8 +2156,8 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
       else if (cs == s.maxsteps) done = true;                // :544-545
       do_reset = done && s.auto_reset;
       if (C.sub == 0) {
-        el<O32>(reward_out, e) = r;
-        el<O32>(done_out, e) = done ? 1 : 0;
+        el<O32>(io.reward_out, e) = r;
+        el<O32>(io.done_out, e) = done ? 1 : 0;
         if (done) {  // the episode record (Utils/utils.py:138-141)
           el<O32>(s.ep_pc, e) = exact1 ? (double)fc / (double)numfree : pc;
           el<O32>(s.ep_len, e) = cs;
@@ -2133,20 +2196,22 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     // writes (one wave: its LDS operations complete in order)
     if constexpr (NT > 64) __syncthreads();
     STAMP(6);
+    reload_state<SH, EPW>(s, io);
     if (!do_reset) {
       store_tiles<NT, EPW, WT, KI, O32>(s, C, I);
       STAMP(7);
     } else {
-      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, nullptr);  // the finished episode's tiles are not stored
+      reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, nullptr, Reload<SH, EPW>());  // the finished episode's tiles are not stored
     }
   } else if (reset_req || sent_reset) {
+    reload_state<SH, EPW>(s, io);
     if (C.sub == 0 && sentinel) {  // the sentinel's done ends the episode (utils.py:22,41)
-      reward_out[e] = 0.0;
-      done_out[e] = 1;
+      io.reward_out[e] = 0.0;
+      io.done_out[e] = 1;
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
-    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, reset_req ? inj_pos : nullptr);
+    reset_env<NT, EPW, WT, SUK, NSM, SH::KN, O32, SH::KM, RPLK>(s, C, reset_req ? io.inj_pos : nullptr, Reload<SH, EPW>());
     dlist = s.dist && C.sub < N;  // fresh maps: M unknown
   } else {
     // sentinel step without auto-reset / env left out of a partial reset:
@@ -2155,6 +2220,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     // plane is scattered.  With the fan march the column planes overlay
     // fold / oold (carve), and a multi-wave slot's column-byte stores would
     // race with another wave's stage_fold stores.
+    reload_state<SH, EPW>(s, io);
     Items<KI> I;
     stage_load<NT, EPW, WT, KI, O32>(s, C, g0, true, I);
     stage_fold<NT, EPW, WT, KI>(s, C, I);
@@ -2162,8 +2228,8 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     // needs the full transform
     dlist = s.dist && C.sub < N && L.dm[C.sub] < 0;
     if (C.sub == 0 && sentinel) {
-      reward_out[e] = 0.0;
-      done_out[e] = 1;
+      io.reward_out[e] = 0.0;
+      io.done_out[e] = 1;
       s.ep_pc[e] = (double)free_old / (double)s.numfree[g0];
       s.ep_len[e] = currstep0;
     }
@@ -2219,15 +2285,16 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(Stat
     }
   }
   STAMP(8);
+  reload_state<SH, EPW>(s, io);
   if constexpr (ObsFast<SH::EGO, SH::N, SH::LC>::ok && (NT == 64 || EPW == 1) &&
                 ObsFast<SH::EGO, SH::N, SH::LC>::NB <= 64) {
-    if (MC_ABL != 4) write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, obs_out);  // every lane of the workgroup
+    if (MC_ABL != 4) write_obs_fast<NT, EPW, WT, SH::N, SH::EGO, SH::LC>(s, C, io.obs_out);  // every lane of the workgroup
   } else {
-    if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 16) ? SH::N : 0>(s, C, obs_out);
+    if (valid) write_obs<NT, EPW, WT, (SH::N > 0 && SH::N <= 16) ? SH::N : 0>(s, C, io.obs_out);
   }
   STAMP(9);
-  if (valid && adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
-    uint8_t* ad = adj_out + (size_t)e * N * N;
+  if (valid && io.adj_out != nullptr) {  // updateCommmunicationGraph (:374-391)
+    uint8_t* ad = io.adj_out + (size_t)e * N * N;
     for (int idx = C.sub; idx < N * N; idx += LPE) {
       const int i = idx / N, j = idx - i * N;
       const int dx = abs(L.x[i] - L.x[j]), dy = abs(L.y[i] - L.y[j]);
@@ -2271,8 +2338,9 @@ static void launch_one(const State& s, int mode, const uint8_t* actions, const u
                        const int32_t* inj_pos, double* reward, uint8_t* done, uint8_t* obs, uint8_t* adj,
                        hipStream_t stream) {
   const size_t slot_lds = state_lds_bytes(s, (int)sizeof(W));
+  const EnvArgs args{s, EnvIO{actions, env_mask, inj_pos, reward, done, obs, adj, mode}};
   hipLaunchKernelGGL((env_kernel<T, P, W, SH>), dim3((s.B + P - 1) / P), dim3(T), slot_stride(slot_lds) * P,
-                     stream, s, mode, actions, env_mask, inj_pos, reward, done, obs, adj);
+                     stream, args);
 }
 
 using Dynamic = Shape<0, 0, 0, 0, 0>;
