@@ -441,10 +441,10 @@ int mc_create(const mc_config* cfg, int hip_device, void** out_env) {
       if (dev_alloc(E, &cc, maps * mc::kDistK * 4) != MC_OK || dev_alloc(E, &cd, maps * mc::kDistK * 4) != MC_OK ||
           dev_alloc(E, &ch, maps * 32) != MC_OK || hipMemset(ch, 0xFF, maps * 32) != hipSuccess ||
           dev_alloc(E, &sm, maps * mc::kDistStrips * 4) != MC_OK || dev_alloc(E, &gk, maps * 8) != MC_OK ||
-          dev_alloc(E, &gc, (size_t)mc::kDistGSlots * 4) != MC_OK || dev_alloc(E, &pc, maps * 4) != MC_OK ||
+          dev_alloc(E, &gc, (size_t)mc::kDistGSlots * mc::kDistGParts * 4) != MC_OK || dev_alloc(E, &pc, maps * 4) != MC_OK ||
           dev_alloc(E, &go, (size_t)mc::kDistGSlots * 4) != MC_OK ||
           dev_alloc(E, &rm, maps * 8) != MC_OK ||
-          dev_alloc(E, &ga, (size_t)mc::kDistGSlots * 4 * mc::kDistK * 8) != MC_OK ||
+          dev_alloc(E, &ga, (size_t)mc::kDistGSlots * mc::kDistGParts * mc::kDistK * 8) != MC_OK ||
           dev_alloc(E, &fl, (maps * 2 + 8) * 4) != MC_OK) {
         std::string msg = g_err;
         mc_destroy(E);

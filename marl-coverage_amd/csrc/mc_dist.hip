@@ -556,11 +556,20 @@ constexpr int kSplitSlots = 512;  // workgroups resident at once (2 per CU)
 #define MC_MAX_PARTS 8
 #endif
 constexpr int kMaxParts = MC_MAX_PARTS;
-constexpr int kGCand = 4 * kDistK;  // candidates a split map's parts may publish (State::dist_gcand)
 // the parts' candidate lists and counts are indexed by the map's full-list
 // index: S > 1 parts only when at most kSplitSlots / 2 maps are on the list
-// (State::dist_gcand was [B][N][kGCand], 2 GB at C5; now 4 MB)
+// (State::dist_gcand was [B][N][4 kDistK], 2 GB at C5).  Round 6: one
+// segment of kDistK per part ([kDistGSlots][kDistGParts][kDistK], 8 MB), so
+// a part publishes its count with a plain store instead of taking its
+// place with a returning atomic (MC_DIST_SEGS=0: one shared list of
+// 4 kDistK, places by atomicAdd)
 static_assert(kDistGSlots == kSplitSlots / 2, "State::dist_gcand's slots");
+static_assert(kMaxParts <= kDistGParts, "State::dist_gcand's segments");
+#ifndef MC_DIST_SEGS
+#define MC_DIST_SEGS 1
+#endif
+constexpr bool kSegs = MC_DIST_SEGS != 0;
+constexpr int kGCand = 4 * kDistK;  // (kSegs = 0) candidates a split map's parts may publish
 #ifndef MC_DIST_FUSED  // build knob (A/B): 0 finalises split maps in a separate mode-3 launch
 #define MC_DIST_FUSED 1
 #endif
@@ -595,6 +604,10 @@ constexpr bool kBalance = MC_DIST_BALANCE != 0;
 // slower (C5 steady 142.5 vs 140.3 us, default window 153.7 vs 151.6 us,
 // profiles/r6/hoab/): off
 constexpr bool kSkipIdle = MC_DIST_SKIP_IDLE != 0;
+#ifndef MC_DIST_STAGE1  // build knob (A/B): 0 keeps the two-pass staging (map rows, then extended rows)
+#define MC_DIST_STAGE1 1
+#endif
+constexpr bool kStage1 = MC_DIST_STAGE1 != 0;
 #ifndef MC_DIST_PARTLIST  // build knob (A/B): 1 = part lists (below); off: measured slower, round 6
 #define MC_DIST_PARTLIST 0
 #endif
@@ -637,13 +650,49 @@ __device__ uint64_t strip_run_mask(const State& s, int pad, uint32_t ea, int the
   return m;
 }
 
+#ifndef MC_DIST_RELOAD  // build knob (A/B): 0 keeps one State for the whole kernel
+#define MC_DIST_RELOAD 1
+#endif
+// The State re-read from the kernel arguments at the item's phase boundaries
+// (as the env kernel's reload_state, mc_env_kernel.hip): the fields a phase
+// uses are loaded there instead of living in SGPRs -- spilled to VGPR lanes,
+// a VALU v_readlane per use -- across the item loop
+struct DistIO {
+  int pad, post;
+  float* pre_out;   // [B][N][8] M, d of the 5 end cells
+  float* dist_obs;  // [B][N][E][E] (POST)
+  const uint32_t* list;
+  uint32_t* count;
+  int mode;
+  uint32_t* full;
+};
+struct DistArgs {
+  State s;
+  DistIO io;
+};
+__device__ __forceinline__ void dist_reload(State& s, DistIO& io) {
+  if constexpr (MC_DIST_RELOAD != 0) {
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();  // the DistArgs
+    asm volatile("" : "+s"(kp));
+    const DistArgs& A = *(const DistArgs*)kp;
+    s = A.s;
+    io = A.io;
+  }
+}
+
 template <int kCL>
-__global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad, int post,
-                                                            float* __restrict__ pre_out,
-                                                            float* __restrict__ dist_obs,
-                                                            const uint32_t* __restrict__ list,
-                                                            uint32_t* __restrict__ count, int mode,
-                                                            uint32_t* __restrict__ full) {
+__global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(DistArgs args) {
+  State s = args.s;
+  DistIO io = args.io;
+  // the arguments as names for the current copy (dist_reload rewrites it)
+  const int& pad = io.pad;
+  const int& post = io.post;
+  float* const& pre_out = io.pre_out;
+  float* const& dist_obs = io.dist_obs;
+  const uint32_t* const& list = io.list;
+  uint32_t* const& count = io.count;
+  const int& mode = io.mode;
+  uint32_t* const& full = io.full;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_cov;
   __shared__ unsigned long long s_key;  // max over the map of (d, distance from the robot, cell)
@@ -720,6 +769,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
 #else
     const int tid = threadIdx.x;
 #endif
+    dist_reload(s, io);
     // modes 2 / 3: the full-list entry (and mode 2's part)
     const uint32_t l = it >> 3;
     const uint32_t fi = mode == 2 ? (xcd ? (l / (uint32_t)S) * 8u + (it & 7u) : it / (uint32_t)S) : (mode == 3 ? it : 0u);
@@ -826,7 +876,18 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       __syncthreads();
       // the parts' candidates: a one-pass list (with theta0), the part lists
       // (without), else none
-      const uint32_t total = ((kOnePass && theta0 > 0) || kPartList) ? ld_ho(s.dist_gcnt + fi, sc1) : 0u;
+      const bool lists = (kOnePass && theta0 > 0) || kPartList;
+      // kSegs: part p's count and segment; pre[p] = the candidates before it
+      uint32_t pre[kMaxParts + 1];
+      pre[0] = 0u;
+      bool over = false;
+#pragma unroll
+      for (int p = 0; p < kMaxParts; ++p) {
+        const uint32_t c = (kSegs && lists && p < S) ? ld_ho(s.dist_gcnt + (size_t)fi * kDistGParts + p, sc1) : 0u;
+        over |= c > (uint32_t)kDistK;
+        pre[p + 1] = pre[p] + (c > (uint32_t)kDistK ? 0u : c);
+      }
+      const uint32_t total = kSegs ? pre[kMaxParts] : (lists ? ld_ho(s.dist_gcnt + fi, sc1) : 0u);
       const unsigned long long gk = ld_ho(s.dist_gkey + ea, sc1);
       const int thr = (int)(gk >> 48) - kDistT;  // the candidates that are cache cells
       // a part list that overflowed and may hold cache cells: the serial pass
@@ -836,9 +897,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
                              : ld_ho(dist_obs + (size_t)ea * E * E + (t - 5), sc1));
       for (int st = tid; st < min(nstrips_all, kMaxTrack); st += kDtThreads)
         s_smax[st] = (int)ld_ho(s.dist_sm + (size_t)ea * kMaxTrack + st, sc1);
-      if (gk != 0 && total <= (uint32_t)kGCand)
+      if (gk != 0 && (kSegs ? !over : total <= (uint32_t)kGCand))
         for (int k = tid; k < (int)total; k += kDtThreads) {
-          const int2 c = ld_ho(s.dist_gcand + (size_t)fi * kGCand + k, sc1);
+          size_t at = (size_t)fi * kGCand + k;
+          if constexpr (kSegs) {  // segment p holds candidates pre[p] .. pre[p + 1] - 1
+            uint32_t base = 0u;
+            int p = 0;
+#pragma unroll
+            for (int q = 1; q < kMaxParts; ++q)
+              if ((uint32_t)k >= pre[q]) {
+                p = q;
+                base = pre[q];
+              }
+            at = ((size_t)fi * kDistGParts + p) * kDistK + ((uint32_t)k - base);
+          }
+          const int2 c = ld_ho(s.dist_gcand + at, sc1);
           if (c.y >= thr) {
             const int j = atomicAdd(&s_ccount, 1);
             if (j < kDistK) {
@@ -851,12 +924,13 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if (tid == 0) {
         s_key = gk;
         s_cov = gk != 0;  // a covered map's key is nonzero (its far or cell field)
-        if (total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
+        if (kSegs ? over : total > (uint32_t)kGCand) s_ccount = kDistK + 1;  // overflowed: the second pass
         if (ovf > 0u && (int)ovf - 1 >= thr) s_ccount = kDistK + 1;
         s.dist_gkey[ea] = 0;  // zero for the map's next split transform
-        s.dist_gcnt[fi] = 0;
+        if (!kSegs) s.dist_gcnt[fi] = 0;
         if (kPartList) s.dist_govf[fi] = 0;
       }
+      if (kSegs && tid < S) s.dist_gcnt[(size_t)fi * kDistGParts + tid] = 0;
       __syncthreads();
     };
     if (mode == 3) {
@@ -865,7 +939,86 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     }
     // the map's row bitboard (Cb) in LDS
     auto stage_cb = [&]() {
-      {
+      if (kStage1 && pad <= 16) {
+        // one pass: a thread takes extended word w of one tile row (8 map
+        // rows), loads the 8 tiles of map word w and the tile pair 8w-2,
+        // 8w-1 (the last pad <= 16 columns of map word w-1, shifted in from
+        // the left), transposes their bytes with v_perm into the 8 rows'
+        // words and writes them, shifted right by pad, straight into the
+        // extended rows pad + 8 ti + r of Cb.  The pad rows above and below
+        // the map are zeroed.  (Round 5's two passes staged map rows in the
+        // strip area first and extended them in a second LDS pass: ~6.8k of
+        // a part's ~16k staging cycles at the C5 steady state,
+        // profiles/r6/stamps/dist_steady.txt.)
+        int any = 0;
+        const int nq = s.TR * RW;
+        for (int q0 = tid; q0 < nq; q0 += 2 * kDtThreads) {
+          uint32_t lo[2][8], hi[2][8], plo[2][2], phi[2][2];  // word w's tiles; tiles 8w-2, 8w-1
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int q = q0 + k * kDtThreads;
+            const int ti = q / RW, w = q - ti * RW;
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              const int tj = 8 * w + j;
+              uint4 t = make_uint4(0u, 0u, 0u, 0u);
+              if (q < nq && tj < s.TC) t = *reinterpret_cast<const uint4*>(free_t + tile_index(s.TCS, ti, tj));
+              if (tj + 1 >= s.TC) t.z = t.w = 0u;
+              lo[k][j] = t.x;
+              hi[k][j] = t.y;
+              lo[k][j + 1] = t.z;
+              hi[k][j + 1] = t.w;
+            }
+            const int tp = 8 * w - 2;  // even: one 16-byte load (both tiles < TC when w <= RWm)
+            uint4 t = make_uint4(0u, 0u, 0u, 0u);
+            if (q < nq && pad > 0 && w > 0 && tp < s.TC) t = *reinterpret_cast<const uint4*>(free_t + tile_index(s.TCS, ti, tp));
+            if (tp + 1 >= s.TC) t.z = t.w = 0u;
+            plo[k][0] = t.x;
+            phi[k][0] = t.y;
+            plo[k][1] = t.z;
+            phi[k][1] = t.w;
+          }
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int q = q0 + k * kDtThreads;
+            if (q >= nq) break;
+            const int ti = q / RW, w = q - ti * RW;
+            const int nr = min(8, s.Wp - 8 * ti);
+            const uint64_t wm = (w == RW - 1) ? last : ~0ull;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              if (r >= nr) break;
+              const uint32_t* src = r < 4 ? lo[k] : hi[k];
+              const uint32_t* psrc = r < 4 ? plo[k] : phi[k];
+              const uint32_t b = (uint32_t)(r & 3);
+              // byte b of src[j]: pairs (j, j + 1) -> bytes 0, 1 of a dword,
+              // then two such pairs -> 4 bytes
+              const uint32_t sel2 = b | ((4u + b) << 8) | 0x0C0C0000u;
+              const uint32_t p01 = __builtin_amdgcn_perm(src[1], src[0], sel2);
+              const uint32_t p23 = __builtin_amdgcn_perm(src[3], src[2], sel2);
+              const uint32_t p45 = __builtin_amdgcn_perm(src[5], src[4], sel2);
+              const uint32_t p67 = __builtin_amdgcn_perm(src[7], src[6], sel2);
+              const uint32_t wlo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+              const uint32_t whi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
+              const uint64_t cur = (uint64_t)wlo | ((uint64_t)whi << 32);
+              // bits 48..63 of map word w - 1 (tiles 8w-2, 8w-1) as 16 bits
+              const uint32_t prev16 = __builtin_amdgcn_perm(psrc[1], psrc[0], sel2);
+              const uint64_t c = (pad > 0 ? ((cur << pad) | (uint64_t)(prev16 >> (16 - pad))) : cur) & wm;
+              Cb[(size_t)(pad + 8 * ti + r) * RW + w] = c;
+              any |= c != 0ull;
+            }
+          }
+        }
+        // the extended rows outside the map
+        const int below = RX - pad - s.Wp;
+        for (int i = tid; i < (pad + below) * RW; i += kDtThreads) {
+          const int row = i / RW;
+          Cb[(size_t)(row < pad ? row : row + s.Wp) * RW + (i - row * RW)] = 0ull;
+        }
+        DSTAMP(tsa);
+        DSTAMP(tsb);
+        if (any) s_cov = 1;
+      } else {
         // the agent's tiles as map rows in the strip area (free until the
         // strips start): a thread takes 8 tiles of one tile row (one 64-column
         // word of 8 map rows), loads them, and transposes their bytes with
@@ -963,6 +1116,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     }
     bool cov = fast || s_cov != 0;
     DSTAMP(ts1);
+    dist_reload(s, io);
 
     // row-pass registers: a thread owns rows tid and tid + kDtThreads
     int lastL[2] = {-kInf, -kInf};  // last covered column left of the strip
@@ -1223,6 +1377,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       strip(st, -1, (kOnePass && theta0 > 0) ? max(max(theta0, runmax) - kDistT, 0) : -1);
     }
     DSTAMP(ts2);
+    dist_reload(s, io);
     const int vmax = bestv >= 0 ? (int)(bestkey >> 16) : -1;
     const int ubest = (int)(bestkey & 0xFFFF), vbest = bestv;
     // witness: of the maxima, the one farthest from the robot (new coverage
@@ -1280,13 +1435,21 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
       if ((kOnePass && theta0 > 0) || part_list) {
         const int n = s_ccount;
         if (n > 0 && (n <= kDistK || theta0 > 0)) {
-          if (tid == 0) s_base = atomicAdd(s.dist_gcnt + fi, (uint32_t)(n <= kDistK ? n : kGCand + 1));
-          __syncthreads();
-          const uint32_t base = s_base;
-          if (n <= kDistK)
-            for (int k = tid; k < n; k += kDtThreads)
-              if (base + k < (uint32_t)kGCand)
-                st_ho(s.dist_gcand + (size_t)fi * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused && kHoSc1);
+          if constexpr (kSegs) {  // this part's segment and count (kDistK + 1: overflowed)
+            const size_t sg = (size_t)fi * kDistGParts + part;
+            if (tid == 0) st_ho(s.dist_gcnt + sg, (uint32_t)min(n, kDistK + 1), kFused && kHoSc1);
+            if (n <= kDistK)
+              for (int k = tid; k < n; k += kDtThreads)
+                st_ho(s.dist_gcand + sg * kDistK + k, make_int2(s_ccell[k], s_cdv[k]), kFused && kHoSc1);
+          } else {
+            if (tid == 0) s_base = atomicAdd(s.dist_gcnt + fi, (uint32_t)(n <= kDistK ? n : kGCand + 1));
+            __syncthreads();
+            const uint32_t base = s_base;
+            if (n <= kDistK)
+              for (int k = tid; k < n; k += kDtThreads)
+                if (base + k < (uint32_t)kGCand)
+                  st_ho(s.dist_gcand + (size_t)fi * kGCand + base + k, make_int2(s_ccell[k], s_cdv[k]), kFused && kHoSc1);
+          }
         }
       }
       if constexpr (kFused) {
@@ -1348,6 +1511,7 @@ __global__ __launch_bounds__(kDtThreads, 4) void dist_kernel_t(State s, int pad,
     }
     // no covered cell: the restatement's convention (-1 everywhere); only the
     // discarded reset-time PRE term can see it
+    dist_reload(s, io);
     const int M = fast ? (int)(s_fkey >> 16) : (cov ? (int)(s_key >> 48) : -1);
     const float Mf = (float)M;
     if (fast) {
@@ -1504,11 +1668,16 @@ size_t dist_static_lds_bytes() {
 constexpr int kFastThreads = MC_FAST_THREADS;
 constexpr int kFastBuf = 128;  // full-list entries a workgroup buffers before one atomic
 
-__global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pad, float* __restrict__ pre_out,
-                                                                 float* __restrict__ dist_obs,
-                                                                 const uint32_t* __restrict__ list,
-                                                                 uint32_t* __restrict__ count,
-                                                                 uint32_t* __restrict__ full) {
+__global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(DistArgs args) {
+  // (DistArgs: post and mode unused; the State and arguments re-read per map,
+  // dist_reload)
+  State s = args.s;
+  DistIO io = args.io;
+  const int& pad = io.pad;
+  float* const& pre_out = io.pre_out;
+  float* const& dist_obs = io.dist_obs;
+  const uint32_t* const& list = io.list;
+  uint32_t* const& full = io.full;
   extern __shared__ __attribute__((aligned(16))) int s_dyn[];  // the targets' d: [5 + E*E]
   __shared__ uint64_t ft[kFastTiles];
   __shared__ uint16_t cdv[kDistK];
@@ -1549,6 +1718,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
     __syncthreads();
     const uint32_t nc = s_nc;
     for (uint32_t j = 0; j < nc; ++j) {
+      dist_reload(s, io);
       const uint32_t ea = s_cl[j];
       uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
       uint64_t tsv[2] = {0, 0};
@@ -1574,6 +1744,7 @@ __global__ __launch_bounds__(kFastThreads) void dist_fast_kernel(State s, int pa
 #endif
       );
       DSTAMP(tm1);
+      dist_reload(s, io);
       const bool served = tried && s_ffail == 0 && (int)(s_fkey >> 16) >= cM0 - kDistT;
       if (served) {
         cache_serve<kFastThreads>(s, T, ea, s_fkey, ccnt, cM0, cdv, s_dyn, pre_out, dist_obs, nullptr);
@@ -1625,8 +1796,8 @@ static hipError_t launch_full(const State& s, int pad, int post, float* pre_out,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
       if (e_ != hipSuccess) return e_;                                                         \
     }                                                                                          \
-    hipLaunchKernelGGL(dist_kernel_t<CL>, dim3(grid), dim3(kDtThreads), lds, stream, s, pad,   \
-                       post, pre_out, dist_obs, list, count, mode, full);                      \
+    hipLaunchKernelGGL(dist_kernel_t<CL>, dim3(grid), dim3(kDtThreads), lds, stream,            \
+                       DistArgs{s, DistIO{pad, post, pre_out, dist_obs, list, count, mode, full}}); \
   } while (0)
   if constexpr (kCh == 64) {
     if (cl == 4) MC_DT(4);
@@ -2023,8 +2194,8 @@ hipError_t launch_dist_listed(const State& s, int pad, float* pre_out, float* di
   if (!full || !s.dist_ch)
     return launch_full(s, pad, 1, pre_out, dist_obs, list, count, grid, 0, nullptr, stream);
   const unsigned fgrid = (unsigned)(maps < MC_FAST_GRID ? maps : MC_FAST_GRID);
-  hipLaunchKernelGGL(dist_fast_kernel, dim3(fgrid), dim3(kFastThreads), (size_t)(5 + s.E * s.E) * 4, stream, s, pad,
-                     pre_out, dist_obs, list, count, full);
+  hipLaunchKernelGGL(dist_fast_kernel, dim3(fgrid), dim3(kFastThreads), (size_t)(5 + s.E * s.E) * 4, stream,
+                     DistArgs{s, DistIO{pad, 1, pre_out, dist_obs, list, count, 1, full}});
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // grids of about the resident workgroups (two per CU); mode 2 has at most

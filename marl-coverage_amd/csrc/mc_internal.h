@@ -152,8 +152,8 @@ struct State {
   uint32_t* dist_sm;
   // with the cache: the split full transform's per-map partials (mc_dist.hip
   // modes 2 / 3; zero between uses): the best key [B][N]; by full-list index
-  // (< kDistGSlots) the candidate cells published and the candidates
-  // [kDistGSlots][4 * kDistK] (cell, d)
+  // (< kDistGSlots) and part (< kDistGParts) the candidate count each part
+  // published and its candidates [kDistGSlots][kDistGParts][kDistK] (cell, d)
   unsigned long long* dist_gkey;
   uint32_t* dist_gcnt;
   // by full-list index: 1 + the largest own maximum of the parts whose
@@ -181,6 +181,7 @@ constexpr int kMaxItemsPerLane = 2;  // staged (agent, tile) items per lane
 #endif
 constexpr int kDistK = MC_DIST_K;    // top-cell cache: cells per map
 constexpr int kDistGSlots = 256;      // full-list entries a split transform can split (mc_dist.hip kSplitSlots / 2)
+constexpr int kDistGParts = 8;        // candidate segments per entry: one per part (mc_dist.hip kMaxParts)
 constexpr int kListShards = 8;        // dist work-list append counters (one address took every env's atomic)
 constexpr int kShardStride = 32;      // u32 words between them (a 128-B line each)
 constexpr int kDistStrips = 64;      // strips whose maxima the cache keeps (extended grids up to 2048 columns)
