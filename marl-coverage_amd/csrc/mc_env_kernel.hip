@@ -55,11 +55,14 @@ struct Scal {
   int32_t grid;
   uint32_t ep;
   int32_t do_reset;
-  int32_t pad_;
+  int32_t path;        // the step's branch flags (kPath*), read back after it
   uint64_t dist_hit;   // dist_reward: agents whose witness cell got closer than M
   uint64_t zero;       // always 0: the merge's dedup reads it for agents whose block misses the tile
 };
 static_assert(sizeof(Scal) <= 64, "Scal must fit its 64-byte LDS slot");
+
+// Scal::path bits
+constexpr int kPathActive = 1, kPathResetReq = 2, kPathSentReset = 4, kPathSentinel = 8;
 
 // the lidar marches by sectors (fan_march) rather than by rays
 __device__ __forceinline__ bool fan_on(const State& s) { return s.sensor == 0 && s.fan_nsec + s.fan_nspec > 0; }
@@ -1500,6 +1503,9 @@ __device__ __forceinline__ void reload_state(State& s) {
 #ifndef MC_RELOAD_INNER  // build knob (A/B): 1 = re-read inside sense_and_merge / reset_env too
 #define MC_RELOAD_INNER 0
 #endif
+#ifndef MC_UNIFORM_FLAGS  // build knob (A/B): 0 keeps the env flags as lane values
+#define MC_UNIFORM_FLAGS 1
+#endif
 template <class SH, int EPW>
 struct Reload {
   __device__ __forceinline__ void operator()(State& s) const {
@@ -1982,8 +1988,12 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
   asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(act_raw), "v"(act0_raw), "v"(req_raw), "v"(g0),
                "v"(bm0.x), "v"(bm0.w), "v"(mwv.x), "v"(mwv.y), "v"(chd.x), "v"(chd.w), "v"(chb.y));
   const int act = is_step ? act_raw : 255;
-  const int act0 = is_step ? act0_raw : 0;      // agent 0's byte: the sentinel
-  const int req = io.env_mask != nullptr ? req_raw : 1;
+  // one env per workgroup: the env's flags are uniform -- made scalar
+  // (readfirstlane), their branches are scalar branches instead of lane masks
+  // kept in SGPR pairs (MC_UNIFORM_FLAGS)
+  auto uni = [](int v) { return (EPW == 1 && MC_UNIFORM_FLAGS) ? __builtin_amdgcn_readfirstlane(v) : v; };
+  const int act0 = uni(is_step ? act0_raw : 0);  // agent 0's byte: the sentinel
+  const int req = uni(io.env_mask != nullptr ? req_raw : 1);
 
   const bool sentinel = valid && is_step && act0 == 255;
   const bool reset_req = valid && !is_step && req != 0;
@@ -2005,6 +2015,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
     L.sc->dist_hit = 0;
     L.sc->dist_fail = 0;
     L.sc->zero = 0;
+    if constexpr (EPW == 1 && MC_UNIFORM_FLAGS)
+      L.sc->path = (active ? kPathActive : 0) | (reset_req ? kPathResetReq : 0) | (sent_reset ? kPathSentReset : 0) |
+                   (sentinel ? kPathSentinel : 0);
   }
   if (s.dist && C.sub < N) {  // dist_reward: M and witness of each free map
     L.dm[C.sub] = mwv.x;
@@ -2097,6 +2110,18 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
     // (compiled shapes; the generic kernels keep the loads in the reward:
     // two more live registers there cost the u64 ones a wave per SIMD)
     constexpr bool kPrePrefetch = SH::N > 0;
+    // one env per workgroup: the env's counters re-read here (they land
+    // during the sensing) rather than kept from round trip 1 in SGPRs,
+    // which spilled (nothing writes them before the reward)
+    uint32_t free_old_r = free_old, vis_old_r = vis_old;
+    int currstep_r = currstep0;
+    double dthresh_r = dthresh0;
+    if constexpr (EPW == 1 && MC_UNIFORM_FLAGS) {
+      free_old_r = el<O32>(s.free_cnt, e);
+      vis_old_r = el<O32>(s.vis_cnt, e);
+      currstep_r = el<O32>(s.currstep, e);
+      dthresh_r = el<O32>(s.done_thresh, e);
+    }
     float dpre0 = 0.0f, dprek = 0.0f;
     if (kPrePrefetch && s.dist && C.sub < N) {
       const int dx = L.x[C.sub] - L.x0[C.sub], dy = L.y[C.sub] - L.y0[C.sub];
@@ -2114,9 +2139,9 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
     bool do_reset;
     {
       Scal* c = L.sc;
-      const uint32_t fc = free_old + c->cnt_free;
-      const uint32_t vc = vis_old + c->cnt_vis;
-      const int cs = currstep0 + 1;                          // :154
+      const uint32_t fc = free_old_r + c->cnt_free;
+      const uint32_t vc = vis_old_r + c->cnt_vis;
+      const int cs = currstep_r + 1;                         // :154
       // observe() :206-258 returns the float32 sum of the agents' distance
       // terms (dist_reward, agent order) plus the union delta (float64)
       // (only lane 0's value is stored: the agents' terms are in the slot's
@@ -2138,7 +2163,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
       }
       const double obs_reward = (double)dsum + (double)c->cnt_vis;
       double r = c->pen + obs_reward;                        // :120,132-151
-      double dt = dthresh0;
+      double dt = dthresh_r;
       const double thr = (1.0 < dt) ? 1.0 : dt;              // min(done_thresh, 1)
       // pc = count/numfree (:552), correctly rounded; thr <= pc.  With thr
       // == 1 (the default) the test is fc >= numfree exactly (counts are
@@ -2154,7 +2179,7 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
       bool done = false;
       if (covered) { dt += s.dincr; done = true; }           // :540-543
       else if (cs == s.maxsteps) done = true;                // :544-545
-      do_reset = done && s.auto_reset;
+      do_reset = uni((int)(done && s.auto_reset)) != 0;
       if (C.sub == 0) {
         el<O32>(io.reward_out, e) = r;
         el<O32>(io.done_out, e) = done ? 1 : 0;
@@ -2236,18 +2261,25 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
   }
   __syncthreads();
 
-  if (active || reset_req || sent_reset) {
+  // the branch flags again, from LDS: one env per workgroup keeps them out of
+  // SGPR pairs across the branch (MC_UNIFORM_FLAGS)
+  const int path = L.sc->path;
+  constexpr bool kPathLds = EPW == 1 && MC_UNIFORM_FLAGS;
+  const bool p_active = kPathLds ? (path & kPathActive) != 0 : active;
+  const bool p_reset_req = kPathLds ? (path & kPathResetReq) != 0 : reset_req;
+  const bool p_sent_reset = kPathLds ? (path & kPathSentReset) != 0 : sent_reset;
+  if (p_active || p_reset_req || p_sent_reset) {
     if (C.sub < N)
       el<O32>(reinterpret_cast<int2*>(s.pos), (uint32_t)e * (uint32_t)N + C.sub) = make_int2(L.x[C.sub], L.y[C.sub]);
     if (C.sub == 0) el<O32>(s.moved, e) = L.sc->moved;
     // dist_reward: a reset map, or one whose witness got closer than M,
     // has an unknown M now (recomputed by the full transform, mc_dist.hip)
     if (s.dist && C.sub < N &&
-        (reset_req || sent_reset || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
+        (p_reset_req || p_sent_reset || L.sc->do_reset || ((L.sc->dist_hit >> C.sub) & 1ull)))
       s.dist_mw[((size_t)e * N + C.sub) * 2] = -1;
     if (s.dist_ch && C.sub < N) {
       int* hp = s.dist_ch + ((size_t)e * N + C.sub) * 8;
-      if (reset_req || sent_reset || L.sc->do_reset) {
+      if (p_reset_req || p_sent_reset || L.sc->do_reset) {
         hp[0] = -1;  // the map was cleared: the cached cells' d are stale
       } else if (chd.x > 0) {  // every newly covered cell lies in the sensing window
         const int x = L.x[C.sub], y = L.y[C.sub], H = s.H;
