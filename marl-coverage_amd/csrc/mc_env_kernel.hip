@@ -1428,6 +1428,80 @@ __device__ __forceinline__ void dist_window_am(const State& s, const Ctx<NT, EPW
   }
 }
 
+#ifndef MC_DIST_AM2  // build knob (A/B): 0 keeps dist_window_am's pass-by-pass loop
+#define MC_DIST_AM2 1
+#endif
+// dist_window_am with the agent count known at compile time (NS): the passes'
+// first row reads (the target's own row: the common answer) are issued
+// together, then the few lanes whose target is not covered scan outward,
+// then the stores -- one LDS latency chain for all passes instead of one per
+// pass
+template <int NT, int EPW, typename WT, int NS>
+__device__ __forceinline__ void dist_window_am2(const State& s, const Ctx<NT, EPW, WT>& C, uint64_t skip) {
+  constexpr int LPE = Ctx<NT, EPW, WT>::LPE;
+  constexpr int APP = LPE / 32;               // agents per pass
+  constexpr int NP = (NS + APP - 1) / APP;    // passes
+  const Lds<WT>& L = C.L;
+  const int E = s.E, T = 5 + E * E, RB = 8 * s.TW;
+  const WT cols = sizeof(WT) == 8 && RB >= 64 ? ~(WT)0 : (WT)(((uint64_t)1 << RB) - 1);
+  const int t = C.sub & 31;
+  if (t >= T) return;
+  int ox, oy;
+  if (t < 5) {
+    ox = (t == 1 ? 1 : (t == 3 ? -1 : 0)) - s.pad;
+    oy = (t == 2 ? 1 : (t == 4 ? -1 : 0)) - s.pad;
+  } else {
+    const int k = t - 5, r = k / E;
+    ox = r - s.ego;
+    oy = k - r * E - s.ego;
+  }
+  int lxv[NP], lyv[NP], bv[NP], dv[NP], Mv[NP];
+  bool on[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int a = p * APP + (C.sub >> 5);
+    const int M = L.dm[a < NS ? a : 0];
+    on[p] = a < NS && !((skip >> a) & 1ull) && M >= 0;
+    Mv[p] = M;
+    const int lx = L.x[a < NS ? a : 0] + ox - 8 * L.bx[a < NS ? a : 0];
+    const int ly = L.y[a < NS ? a : 0] + oy - 8 * L.by[a < NS ? a : 0];
+    lxv[p] = lx;
+    lyv[p] = ly;
+    bv[p] = min(min(lx, RB - 1 - lx), min(ly, RB - 1 - ly)) + 1;  // <= 0: outside the block
+    dv[p] = bv[p] + 1;
+    if (on[p] && bv[p] > 0) dv[p] = min(dv[p], row_dist<WT>(L.fpr[row_word<WT>(s, a, lx)] & cols, ly));
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int a = p * APP + (C.sub >> 5);
+    if (on[p] && bv[p] > 0) {
+      const int lx = lxv[p], ly = lyv[p];
+      int d = dv[p];
+      for (int dr = 1; dr < d; ++dr) {
+        if (lx - dr >= 0) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx - dr)] & cols, ly));
+        if (lx + dr < RB) d = min(d, dr + row_dist<WT>(L.fpr[row_word<WT>(s, a, lx + dr)] & cols, ly));
+      }
+      dv[p] = d;
+    }
+  }
+  float* pre_e = const_cast<float*>(s.dist_pre) + (size_t)C.e * NS * 8;
+  float* obs_e = s.dist_obs_out + (size_t)C.e * NS * E * E;
+  uint64_t fail = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int a = p * APP + (C.sub >> 5);
+    if (!on[p]) continue;
+    if (dv[p] > bv[p]) {
+      fail |= 1ull << a;
+      continue;
+    }
+    if (t < 5) pre_e[a * 8 + 1 + t] = (float)dv[p];
+    else obs_e[a * E * E + (t - 5)] = dist_value((float)dv[p], (float)Mv[p]);
+    if (t == 0) pre_e[a * 8] = (float)Mv[p];
+  }
+  if (fail) atomicOr((unsigned long long*)&L.sc->dist_fail, fail);
+}
+
 template <bool O32>
 __device__ __forceinline__ void st_tile(uint64_t* base, uint32_t idx, uint64_t v) {
   if constexpr (O32) *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(base) + (size_t)(idx << 3)) = v;
@@ -2208,8 +2282,13 @@ __global__ __launch_bounds__(NT, (env_min_waves<NT, SH>())) void env_kernel(EnvA
         // row's covered set by a bit-parallel dilation -- 83.6 against 81.7
         // us at the C5 steady state, profiles/r5/win/; removed)
         if constexpr (Ctx<NT, EPW, WT>::LPE % 32 == 0 && MC_DIST_AM) {
-          if (5 + s.E * s.E <= 32) dist_window_am<NT, EPW, WT>(s, C, skip);
-          else dist_window<NT, EPW, WT>(s, C, skip);
+          if constexpr (MC_DIST_AM2 && SH::N > 0 && SH::N <= 64) {
+            if (5 + s.E * s.E <= 32) dist_window_am2<NT, EPW, WT, SH::N>(s, C, skip);
+            else dist_window<NT, EPW, WT>(s, C, skip);
+          } else {
+            if (5 + s.E * s.E <= 32) dist_window_am<NT, EPW, WT>(s, C, skip);
+            else dist_window<NT, EPW, WT>(s, C, skip);
+          }
         } else {
           dist_window<NT, EPW, WT>(s, C, skip);
         }
