@@ -527,6 +527,9 @@ __device__ __forceinline__ void zero_marks(const State& s, const Ctx<NT, EPW, WT
 
 // tile (ti, tj) of agent a gathered from a row plane (the inverse scatter):
 // byte r of the tile = byte tj of word w0 + r * rs (row 8 ti + r; rs = N)
+#ifndef MC_GATHER_BYTES  // build knob (A/B): 0 extracts byte tj of 64-bit rows by shifts
+#define MC_GATHER_BYTES 1
+#endif
 template <typename WT>
 __device__ __forceinline__ uint64_t gather_tile(const WT* rows, int w0, int rs, int tj) {
   if constexpr (sizeof(WT) == 4) {
@@ -538,6 +541,22 @@ __device__ __forceinline__ uint64_t gather_tile(const WT* rows, int w0, int rs, 
       h[q] = __builtin_amdgcn_perm((uint32_t)rows[w0 + (2 * q + 1) * rs], (uint32_t)rows[w0 + 2 * q * rs], sel);
     const uint32_t lo = __builtin_amdgcn_perm(h[1], h[0], 0x05040100u);
     const uint32_t hi = __builtin_amdgcn_perm(h[3], h[2], 0x05040100u);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+  } else if constexpr (MC_GATHER_BYTES != 0) {
+    // 64-bit rows: byte tj of the 8 rows by byte loads (the stage's scatter
+    // writes them the same way), packed by v_perm -- instead of a 64-bit
+    // shift, a mask and a 64-bit shift-or per row
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows + w0) + tj;
+    const int rsb = rs * (int)sizeof(WT);
+    uint32_t b[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) b[r] = rb[r * rsb];
+    const uint32_t p01 = __builtin_amdgcn_perm(b[1], b[0], 0x0C0C0400u);
+    const uint32_t p23 = __builtin_amdgcn_perm(b[3], b[2], 0x0C0C0400u);
+    const uint32_t p45 = __builtin_amdgcn_perm(b[5], b[4], 0x0C0C0400u);
+    const uint32_t p67 = __builtin_amdgcn_perm(b[7], b[6], 0x0C0C0400u);
+    const uint32_t lo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+    const uint32_t hi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
     return (uint64_t)lo | ((uint64_t)hi << 32);
   } else {
     uint64_t t = 0;
